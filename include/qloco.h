@@ -1,0 +1,209 @@
+/*
+ * qloco.h -- C ABI of the MI355X-native batched convex-MPC solver
+ * (libqloco.so).  Plain pointers and sizes only; no torch / Eigen types.
+ *
+ * Every entry point below replaces one interface of the reference
+ * (jtdingx/quadrupedal_loco, paths relative to its root) and is batched over
+ * independent instances.  Device entry points take DEVICE pointers that are
+ * already resident in HBM plus a hipStream_t (passed as void*; NULL = the
+ * default stream); they only enqueue work and return immediately.  Host
+ * entry points (suffix _host) take host pointers and block.
+ *
+ * Layout conventions
+ *  - instance-major ("AoS per field"): field f of instance b lives at
+ *    ptr[b * len(f) + k]; one instance's data is contiguous, so the one
+ *    wavefront that owns the instance reads it with coalesced loads.
+ *  - small matrices mirror Eigen's default column-major storage.
+ *  - SRBD leg order is ConvexMpc's FL, FR, RL, RR (A1CtrlStates.h:44-46);
+ *    force-QP leg order is the Go1 servo's FR, FL, RR, RL (servo.cpp:1054-1058).
+ *
+ * Errors: every function returns a qloco_status (0 = success).  Per-instance
+ * solver outcomes go to the status[] arrays, mirroring QPBaseClass::solveQP
+ * (QPBaseClass.cpp:200-227), which reports failure only through NaN in X.
+ */
+#ifndef QLOCO_H
+#define QLOCO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QLOCO_ABI_VERSION 1
+
+typedef enum qloco_status {
+  QLOCO_OK = 0,
+  QLOCO_MAX_ITER = 1,          /* ADMM hit max_iter (OSQP_MAX_ITER_REACHED)          */
+  QLOCO_INFEASIBLE = 2,        /* EiQuadProg returned +inf (EiQuadProg.cpp:394-400)   */
+  QLOCO_NAN = 3,               /* non-finite solution                                 */
+  QLOCO_BAD_SIZE = 4,          /* sizes outside the compiled limits                   */
+  QLOCO_NOT_PD = 5,            /* Cholesky failed (EiQuadProg.cpp:507-510)            */
+  QLOCO_DEGENERATE = 6,        /* dependent equalities (EiQuadProg.cpp:270-275)       */
+  QLOCO_UB_PATH = 7,           /* reference reads an uninitialised index (:105-110)   */
+  QLOCO_SOLVED_INACCURATE = 8, /* OSQP_SOLVED_INACCURATE                              */
+  QLOCO_ERR_ARG = 100,         /* invalid argument (call-level)                       */
+  QLOCO_ERR_DEVICE = 101,      /* HIP runtime error (call-level)                      */
+  QLOCO_ERR_NO_GPU = 102       /* no gfx950 device visible                            */
+} qloco_status;
+
+const char *qloco_status_string(int status);
+int qloco_abi_version(void);
+/* last HIP error string of the calling thread (empty if none) */
+const char *qloco_last_error(void);
+
+/* ====================================================================== */
+/* 1. SRBD convex MPC (Go1, N-step horizon, 12 contact forces)             */
+/*    replaces ConvexMpc (a1_cpp_open_source/src/ConvexMpc.h:22-94,        */
+/*    ConvexMpc.cpp:8-264) + the OSQP solve in                             */
+/*    A1RobotControl::compute_grf (A1RobotControl.cpp:452-600)             */
+/* ====================================================================== */
+typedef struct qloco_srbd_spec {
+  int32_t horizon;           /* N = PLAN_HORIZON (A1Params.h:26)                   */
+  int32_t feet_per_step;     /* 0: feet[12] per instance (compute_grf); 1: [12N]   */
+  int32_t contacts_per_step; /* 0: contacts[4] (ConvexMpc.cpp:232-249); 1: [4N]    */
+  int32_t output_frame;      /* 0: u0 = QP solution (world);                        */
+                             /* 1: R^T u0 per leg (compute_grf return, :596-599)    */
+  float dt;                  /* mpc_dt = 0.0025 (A1RobotControl.cpp:469)            */
+  float mass;                /* robot_mass                                           */
+  float inertia[9];          /* trunk inertia, col-major                             */
+  float q_weights[13];       /* ConvexMpc ctor q_weights_ (Q = diag(2q))             */
+  float r_weights[12];       /* r_weights_ (R = diag(2r))                            */
+  float mu;                  /* 0.3 (ConvexMpc.cpp:9)                                */
+  float fz_min, fz_max;      /* 0 / 180 (ConvexMpc.cpp:227-228)                      */
+  /* ADMM settings: OSQP names and defaults */
+  float rho, sigma, alpha, eps_abs, eps_rel;
+  int32_t max_iter, check_termination, scaling, adaptive_rho, adaptive_rho_interval;
+  float adaptive_rho_tolerance;
+  int32_t warm_start;        /* 1: read x/y warm start from d_warm (OSQP warm_start) */
+  int32_t polish;            /* 1: OSQP-style solution polishing after ADMM          */
+  int32_t reserved[6];
+} qloco_srbd_spec;
+
+/* Go1 SRBD constants + OSQP default settings. */
+void qloco_srbd_spec_default(qloco_srbd_spec *spec);
+
+/* Largest horizon / stance-variable count the compiled kernels accept. */
+int qloco_srbd_max_stance_vars(void);
+
+/* Batched build + ADMM solve (the hot path).  Device pointers:
+ *   x0[B*13]        mpc_states: [rpy, p, omega, v, -9.8]   (A1RobotControl.cpp:459-463)
+ *   x_ref[B*13N]    mpc_states_d                             (:480-497)
+ *   feet[B*12] or [B*12N]  foot_pos_abs, 3 per leg (FL,FR,RL,RR)
+ *   contacts[B*4] or [B*4N] uint8 0/1
+ * Outputs (NULL = not wanted, except u0):
+ *   u0[B*12]        first-step forces (frame per spec->output_frame)
+ *   u[B*12N]        full solution (world frame)
+ *   status[B], iters[B] (ADMM iterations), obj[B] (QP objective)
+ *   warm[B*(12N+20N)] in/out x|y warm-start state when spec->warm_start. */
+int qloco_srbd_solve(const qloco_srbd_spec *spec, int64_t batch, const float *x0,
+                     const float *x_ref, const float *feet, const uint8_t *contacts,
+                     float *u0, float *u, int32_t *status, int32_t *iters, float *obj,
+                     float *warm, void *stream);
+
+/* Batched condensed-QP build only (ConvexMpc::calculate_qp_mats, dense,
+ * as the reference materialises it).  Outputs per instance (NULL = skip):
+ *   H[B*(12N)^2] col-major, g[B*12N], lb[B*20N], ub[B*20N] (+-1e30 = INFTY),
+ *   Aqp[B*13N*13], Bqp[B*13N*12N] col-major. */
+int qloco_srbd_build(const qloco_srbd_spec *spec, int64_t batch, const float *x0,
+                     const float *x_ref, const float *feet, const uint8_t *contacts,
+                     float *H, float *g, float *lb, float *ub, float *Aqp, float *Bqp,
+                     void *stream);
+
+/* Deterministic synthetic instances, host memory.
+ * gait: 0 trot, 1 pace (reference gait_mode 101), 2 mixed per-step, 3 stance.
+ * x_ref must hold count*13N floats, contacts count*4N bytes. */
+int qloco_gen_srbd_host(uint64_t seed, int32_t horizon, float dt, int32_t gait,
+                        int64_t first, int64_t count, float *x0, float *x_ref,
+                        float *feet, uint8_t *contacts);
+
+/* ====================================================================== */
+/* 2. Dense small-QP active-set solver (Goldfarb-Idnani), batched.          */
+/*    replaces QPsolver_EiQuadProg::solve -> Eigen::QP::solve_quadprog      */
+/*    (rt_mpc_qp/src/QP/QPBaseClass.cpp:36-58; EiQuadProg.cpp:172-513),     */
+/*    quirk-compatible.  Double precision.              */
+/*    n <= 16, p <= 16, m <= 64.  Matrices col-major, per instance:         */
+/*    G[n*n] (only the lower triangle is read), g0[n], CE[n*p], ce0[p],     */
+/*    CI[n*m], ci0[m].  A NULL CE/ce0/CI/ci0 with stride 0 broadcasts one    */
+/*    shared copy; *_stride = elements between instances (0 = shared).     */
+/*    Outputs x[B*n], f[B] (cost, +inf when infeasible), status[B],         */
+/*    iters[B].                                                             */
+/* ====================================================================== */
+int qloco_eiquadprog_solve(int32_t n, int32_t p, int32_t m, int64_t batch, const double *G,
+                           int64_t G_stride, const double *g0, int64_t g0_stride,
+                           const double *CE, int64_t CE_stride, const double *ce0,
+                           int64_t ce0_stride, const double *CI, int64_t CI_stride,
+                           const double *ci0, int64_t ci0_stride, double *x, double *f,
+                           int32_t *status, int32_t *iters, void *stream);
+int qloco_max_gi_vars(void);
+
+/* ====================================================================== */
+/* 3. Go1 force-distribution QP, batched                                    */
+/*    replaces Dynamiccclass::force_distribution + force_opt               */
+/*    (go1_rt_control/src/whole_body_dynamics/dynmics_compute.cpp:141-373, */
+/*    called at servo.cpp:1224-1228 and torque_mode.cpp:1364-1367)          */
+/* ====================================================================== */
+typedef struct qloco_force_params {
+  double mass;    /* 12    dynmics_compute.cpp:31 */
+  double alpha;   /* 1e4   :61 */
+  double beta;    /* 1e3   :62 */
+  double gamma;   /* 10    :63 */
+  double fz_max;  /* 160   :64 */
+  double mu;      /* 0.25 sim (:65), 0.5 HW copy */
+} qloco_force_params;
+void qloco_force_params_default(qloco_force_params *p);
+
+/* Per-instance inputs (device, double):
+ *   com_des[B*3], leg_des[B*12], F_force_des[B*6], rfoot_des[B*3],
+ *   lfoot_des[B*3]      -> force_distribution arguments
+ *   base_p[B*3], feet_p[B*12] (FR,FL,RR,RL), FT_total_des[B*6] -> force_opt
+ *   mode[B], right_support[B] (int32), y_coef[B]
+ * Per-instance state (in/out, double): F_leg_ref[B*12] (3x4 col-major),
+ *   grf_opt[B*12] (previous solution = F_prev of q_goal, :305).
+ * Outputs: F_leg_guess[B*12], qp_solution[B] (int32, 1 = no NaN),
+ *   status[B] (EiQuadProg outcome), iters[B]. */
+int qloco_force_qp_solve(const qloco_force_params *prm, int64_t batch, const double *com_des,
+                         const double *leg_des, const double *F_force_des,
+                         const double *rfoot_des, const double *lfoot_des,
+                         const double *base_p, const double *feet_p,
+                         const double *FT_total_des, const int32_t *mode,
+                         const int32_t *right_support, const double *y_coef,
+                         double *F_leg_ref, double *grf_opt, double *F_leg_guess,
+                         int32_t *qp_solution, int32_t *status, int32_t *iters,
+                         void *stream);
+
+/* Joint torques tau = -J^T F + g_comp (stance) or PD (swing),
+ * Dynamiccclass::compute_joint_torques (dynmics_compute.cpp:109-138), for
+ * all 4 legs of B instances.  Jaco[B*4*9] col-major per leg, swing[B*4],
+ * p_des/p_est/pv_des/pv_est[B*12], F_leg_ref[B*12] -> tau[B*12]. */
+int qloco_joint_torques(int64_t batch, const double *Jaco, const int32_t *swing,
+                        const double *p_des, const double *p_est, const double *pv_des,
+                        const double *pv_est, const double *F_leg_ref, double *tau,
+                        void *stream);
+
+/* ====================================================================== */
+/* 4. rt body-inclination MPC step, batched                                 */
+/*    replaces PRMPCClass::body_theta_mpc (rt_mpc_qp/src/FastMPC/          */
+/*    PRMPCClass.cpp:379-714) called at gait_fast.cpp:620                  */
+/* ====================================================================== */
+/* Per-instance state record (double[32]), created by qloco_body_state_init:
+ *   [0:2] thetaxk  [2:4] thetayk  [4:12] V_ini  [12:26] last com_traj
+ *   [26] bjx1 [27] bjx2 [28] t_yu [29] qp_solution [30:32] reserved        */
+#define QLOCO_BODY_STATE_LEN 32
+int qloco_body_state_init_host(int64_t batch, double *state);
+/* i[B] (loop counter, int32), bodyangle_state[B*4], zmp_ref/angle_ref/
+ * rfoot_ref/lfoot_ref[B*10] (Eigen 2x5 col-major), comacc_ref[B*15] (3x5)
+ * -> com_traj[B*14]; state in/out; status[B] EiQuadProg outcome. */
+int qloco_body_mpc_step(int64_t batch, const int32_t *i, const double *bodyangle_state,
+                        const double *zmp_ref, const double *angle_ref,
+                        const double *rfoot_ref, const double *lfoot_ref,
+                        const double *comacc_ref, double *state, double *com_traj,
+                        int32_t *status, void *stream);
+/* PRMPCClass::Indexfind (PRMPCClass.cpp:716-738) on B fp64 times -> int32 */
+int qloco_body_indexfind(int64_t batch, const double *t, int32_t *j_period, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QLOCO_H */

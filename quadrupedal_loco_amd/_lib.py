@@ -1,0 +1,111 @@
+"""ctypes binding of libqloco.so (the C ABI in include/qloco.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no
+gfx950 device is visible, calls raise instead of computing anything on the
+host.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libqloco.so")
+
+_lib = None
+
+
+class SrbdSpec(C.Structure):
+    """Mirror of `qloco_srbd_spec` (include/qloco.h)."""
+    _fields_ = [
+        ("horizon", C.c_int32), ("feet_per_step", C.c_int32),
+        ("contacts_per_step", C.c_int32), ("output_frame", C.c_int32),
+        ("dt", C.c_float), ("mass", C.c_float), ("inertia", C.c_float * 9),
+        ("q_weights", C.c_float * 13), ("r_weights", C.c_float * 12),
+        ("mu", C.c_float), ("fz_min", C.c_float), ("fz_max", C.c_float),
+        ("rho", C.c_float), ("sigma", C.c_float), ("alpha", C.c_float),
+        ("eps_abs", C.c_float), ("eps_rel", C.c_float),
+        ("max_iter", C.c_int32), ("check_termination", C.c_int32), ("scaling", C.c_int32),
+        ("adaptive_rho", C.c_int32), ("adaptive_rho_interval", C.c_int32),
+        ("adaptive_rho_tolerance", C.c_float), ("warm_start", C.c_int32),
+        ("polish", C.c_int32), ("reserved", C.c_int32 * 6),
+    ]
+
+
+class ForceParams(C.Structure):
+    """Mirror of `qloco_force_params`."""
+    _fields_ = [(k, C.c_double) for k in ("mass", "alpha", "beta", "gamma", "fz_max", "mu")]
+
+
+vp = C.c_void_p
+i64 = C.c_int64
+i32 = C.c_int32
+
+# name -> (restype, argtypes); every symbol include/qloco.h declares
+SIGNATURES = {
+    "qloco_status_string": (C.c_char_p, [C.c_int]),
+    "qloco_abi_version": (C.c_int, []),
+    "qloco_last_error": (C.c_char_p, []),
+    "qloco_srbd_spec_default": (None, [C.POINTER(SrbdSpec)]),
+    "qloco_srbd_max_stance_vars": (C.c_int, []),
+    "qloco_srbd_solve": (C.c_int, [C.POINTER(SrbdSpec), i64, vp, vp, vp, vp, vp, vp, vp, vp,
+                                   vp, vp, vp]),
+    "qloco_srbd_solve_ex": (C.c_int, [C.POINTER(SrbdSpec), i64, vp, vp, vp, vp, vp, vp, vp, vp,
+                                      vp, vp, vp, i32, vp]),
+    "qloco_srbd_build": (C.c_int, [C.POINTER(SrbdSpec), i64, vp, vp, vp, vp, vp, vp, vp, vp,
+                                   vp, vp, vp]),
+    "qloco_gen_srbd_host": (C.c_int, [C.c_uint64, i32, C.c_float, i32, i64, i64, vp, vp, vp,
+                                      vp]),
+    "qloco_eiquadprog_solve": (C.c_int, [i32, i32, i32, i64, vp, i64, vp, i64, vp, i64, vp, i64,
+                                         vp, i64, vp, i64, vp, vp, vp, vp, vp]),
+    "qloco_max_gi_vars": (C.c_int, []),
+    "qloco_force_params_default": (None, [C.POINTER(ForceParams)]),
+    "qloco_force_qp_solve": (C.c_int, [C.POINTER(ForceParams), i64] + [vp] * 18),
+    "qloco_joint_torques": (C.c_int, [i64] + [vp] * 9),
+    "qloco_body_state_init_host": (C.c_int, [i64, vp]),
+    "qloco_body_mpc_step": (C.c_int, [i64] + [vp] * 10),
+    "qloco_body_indexfind": (C.c_int, [i64, vp, vp, vp]),
+}
+
+
+class QlocoError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libqloco.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise QlocoError(
+                "libqloco.so not built (%s); run `python -m quadrupedal_loco_amd.build` "
+                "or __graft_entry__.build()" % LIB_PATH)
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            if not hasattr(L, name):
+                continue  # reported by missing_symbols()
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def missing_symbols():
+    L = lib()
+    return [n for n in SIGNATURES if not hasattr(L, n)]
+
+
+def check(status, what):
+    if status != 0:
+        L = lib()
+        msg = L.qloco_status_string(status).decode()
+        err = L.qloco_last_error().decode()
+        raise QlocoError("%s failed: %s %s" % (what, msg, err))
+
+
+def ptr(t):
+    """Device (or host) address of a torch tensor / numpy array, or None."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return C.c_void_p(t.data_ptr())
+    return C.c_void_p(t.ctypes.data)

@@ -1,0 +1,74 @@
+"""Build libqloco.so (HIP, gfx950) in-tree with hipcc.
+
+No cmake / JIT: one hipcc line per translation unit, objects cached by
+mtime under quadrupedal_loco_amd/lib/obj/, linked into
+quadrupedal_loco_amd/lib/libqloco.so (git-ignored, travels to the GPU box).
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+OBJDIR = os.path.join(LIBDIR, "obj")
+LIB = os.path.join(LIBDIR, "libqloco.so")
+INCLUDE = os.path.join(ROOT, "include")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+SOURCES = [
+    "qloco_capi.hip",
+    "qloco_srbd.hip",
+    "qloco_gen.cpp",
+]
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC]
+
+
+def _needs(obj, deps):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose=False, jobs=8):
+    os.makedirs(OBJDIR, exist_ok=True)
+    headers = [os.path.join(INCLUDE, "qloco.h")] + [
+        os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    cmds, objs = [], []
+    for src in SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(OBJDIR, src + ".o")
+        objs.append(obj)
+        if not _needs(obj, [path] + headers):
+            continue
+        if src.endswith(".hip"):
+            cmd = [HIPCC, "--offload-arch=" + ARCH, "-x", "hip"] + COMMON + ["-c", path, "-o", obj]
+        else:  # host-only C++ (generator): exact IEEE, no contraction
+            cmd = [HIPCC, "-x", "c++"] + COMMON + ["-ffp-contract=off", "-c", path, "-o", obj]
+        cmds.append(cmd)
+    procs = []
+    for cmd in cmds:
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        while len([p for _, p in procs if p.poll() is None]) >= jobs:
+            procs[0][1].wait()
+    for cmd, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            sys.stderr.write(out.decode())
+            raise RuntimeError("hipcc failed: " + " ".join(cmd))
+    if cmds or not os.path.exists(LIB) or _needs(LIB, objs):
+        link = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        if verbose:
+            print(" ".join(link))
+        subprocess.run(link, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

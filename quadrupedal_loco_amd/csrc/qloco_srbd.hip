@@ -1,0 +1,989 @@
+// qloco_srbd.hip -- batched SRBD convex MPC for gfx950 (MI355X).
+//
+// Replaces the reference's per-call ConvexMpc build + OSQP solve
+// (a1_cpp_open_source/src/ConvexMpc.cpp:8-264, A1RobotControl.cpp:452-600)
+// with ONE fused kernel: one QP instance per workgroup of W wavefronts
+// (W = 1 for <= 63 stance variables, W = 2 for <= 126), nothing but the
+// inputs and the solution touching HBM.
+//
+// Design (DESIGN.md §3 has the derivation):
+//  * Swing legs are eliminated exactly: their bounds fz in [0, 0] with the
+//    friction rows force f = 0, so only stance forces are variables
+//    (n = 3 * #stance (step, leg) pairs, 5 constraint rows per stance leg).
+//  * The condensed Hessian H = Bqp' Q Bqp + R is generated in closed form.
+//    With forward Euler and the reference's A_c (ConvexMpc.cpp:111-133),
+//    A_c is nilpotent, so A_d^k B_d = B_d + k dt A_c B_d and every B_qp
+//    block is b + (i-j) e with b (rows 6..11) and e (rows 0..5) disjoint:
+//    H[r][c] = K0(j_r,j_c) * <b_r,b_c>_Q + K2(j_r,j_c) * <e_r,e_c>_Q + R,
+//    K0 = #{i >= max(j_r,j_c)}, K2 = sum_i (i-j_r)(i-j_c).  Bqp x and
+//    Bqp' w (gradient, dual residual) are prefix/suffix sums over steps.
+//  * ADMM is OSQP's algorithm (Ruiz scaling, rho vector, relaxation,
+//    termination every check_termination iterations, adaptive rho) in fp32.
+//    Lane v owns stance variable v (leg triples never straddle a wave:
+//    21 legs = 63 lanes per wave, lane 63 idles), its row of K^-1 in VGPRs
+//    (K = P + sigma I + A' diag(rho) A, inverted by Gauss-Jordan with a
+//    wave-uniform pivot index -> s_set_gpr_idx, no scratch), and the <= 2
+//    constraint rows of its leg's 5 (x: rows 0,1; y: rows 2,3; z: row 4).
+//    Per iteration: one LDS broadcast of the KKT right-hand side, one
+//    64-wide matvec against the register-resident K^-1, three lane shuffles.
+#include <math.h>
+#include <string.h>
+
+#include "qloco_common.hpp"
+
+namespace qloco {
+
+constexpr int kMaxN = 20;    // max horizon compiled in (BASELINE configs: N <= 20)
+constexpr int kLegsPerWave = 21;
+
+struct SrbdArgs {
+  int N, feet_per_step, contacts_per_step, output_frame;
+  float dt, mass;
+  float inertia[9];
+  float q2[13];  // 2 * q_weights (Q diagonal, ConvexMpc.cpp:18-24)
+  float r2[12];  // 2 * r_weights (R diagonal, :38-45)
+  float mu, fz_min, fz_max;
+  float rho, sigma, alpha, eps_abs, eps_rel;
+  int max_iter, check_termination, scaling, adaptive_rho, rho_interval;
+  float rho_tol;
+  int warm_start, polish;
+  int64_t batch;
+  const float *x0, *xref, *feet;
+  const uint8_t *contacts;
+  float *u0, *u, *obj, *warm;
+  int *status, *iters, *rho_updates;
+};
+
+typedef float v32f __attribute__((ext_vector_type(32)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f8v __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef int i2v __attribute__((ext_vector_type(2)));
+
+// One register row of K / K^-1: separate vector members (never an array of
+// vectors) and no dynamically-indexed element stores, so SROA keeps the row
+// in VGPRs; dynamic (wave-uniform) element reads lower to s_set_gpr_idx.
+template <int W>
+struct Row;
+template <>
+struct Row<1> {
+  v32f k0, k1;
+  __device__ __forceinline__ float get(int c) const {
+    const int e = c & 31;
+    const float a0 = k0[e], a1 = k1[e];
+    return (c >> 5) == 0 ? a0 : a1;
+  }
+  __device__ __forceinline__ void set(int c, float x) {
+    if ((c >> 5) == 0) k0[c & 31] = x;
+    else k1[c & 31] = x;
+  }
+  __device__ __forceinline__ void scale(float s) { k0 *= s; k1 *= s; }
+  __device__ __forceinline__ void zero() { k0 = (v32f)(0.0f); k1 = (v32f)(0.0f); }
+};
+template <>
+struct Row<2> {
+  v32f k0, k1, k2, k3;
+  __device__ __forceinline__ float get(int c) const {
+    const int ch = c >> 5, e = c & 31;
+    const float a0 = k0[e], a1 = k1[e], a2 = k2[e], a3 = k3[e];
+    return ch == 0 ? a0 : (ch == 1 ? a1 : (ch == 2 ? a2 : a3));
+  }
+  __device__ __forceinline__ void set(int c, float x) {
+    const int ch = c >> 5, e = c & 31;
+    if (ch == 0) k0[e] = x;
+    else if (ch == 1) k1[e] = x;
+    else if (ch == 2) k2[e] = x;
+    else k3[e] = x;
+  }
+  __device__ __forceinline__ void scale(float s) { k0 *= s; k1 *= s; k2 *= s; k3 *= s; }
+  __device__ __forceinline__ void zero() {
+    k0 = (v32f)(0.0f); k1 = (v32f)(0.0f); k2 = (v32f)(0.0f); k3 = (v32f)(0.0f);
+  }
+};
+
+template <int W>
+struct SrbdLds {
+  static constexpr int NC = 64 * W;  // register-row length (columns)
+  float x0[16];
+  float err[13 * kMaxN];     // scratch for gradient / P x
+  float W0[13 * kMaxN];      // suffix sums  sum_{i>=j} w_i
+  float W1[13 * kMaxN];      //              sum_{i>=j} (i-j) w_i
+  float agg[12 * kMaxN];     // per-step aggregates of coef * x
+  float bv[NC][8];           // per var: coef b(6..8), e(0..2), step, comp
+  float bc[2][NC];           // broadcast ring (matvec rhs, pivots, D)
+  float xs[NC];              // unscaled x per var (for P x)
+  float piv[2];              // pivot values of the GJ ring
+  float red[W][16];          // cross-wave reduction slots
+  int legtab[4 * kMaxN];     // stance pair -> 4*step + leg
+  int stepstart[kMaxN + 1];  // first stance pair of each step
+  uint8_t ct[4 * kMaxN];
+  int nlegs;
+};
+
+// K0 / K2 horizon sums for the closed-form Hessian (see header comment)
+__device__ __forceinline__ void k0k2(int ja, int jb, int N, float &K0, float &K2) {
+  int M = ja > jb ? ja : jb;
+  int T = N - M;
+  int al = M - ja, be = M - jb;
+  int S1 = T * (T - 1) / 2;
+  int S2 = (T - 1) * T * (2 * T - 1) / 6;
+  K0 = (float)T;
+  K2 = (float)(S2 + (al + be) * S1 + al * be * T);
+}
+
+// Block-wide max/sum of NVAL values (all threads get the result).
+template <int W, int NVAL>
+__device__ __forceinline__ void block_reduce(float (&v)[NVAL], const bool (&is_sum)[NVAL],
+                                             float (*red)[16]) {
+#pragma unroll
+  for (int k = 0; k < NVAL; ++k) v[k] = is_sum[k] ? wave_sum(v[k]) : wave_max(v[k]);
+  if (W > 1) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < NVAL; ++k) red[wave][k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NVAL; ++k) {
+      float r = red[0][k];
+#pragma unroll
+      for (int w = 1; w < W; ++w) r = is_sum[k] ? (r + red[w][k]) : fmaxf(r, red[w][k]);
+      v[k] = r;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < NVAL; ++k) v[k] = uni(v[k]);
+}
+
+// coefficient of stance variable (bv entry) on condensed-state row s (0..11)
+__device__ __forceinline__ float coef_row(const float *bvc, int s, float dtm, float dt2m) {
+  const int comp = (int)bvc[7];
+  if (s < 3) return bvc[3 + s];
+  if (s < 6) return (comp == s - 3) ? dt2m : 0.0f;
+  if (s < 9) return bvc[s - 6];
+  return (comp == s - 9) ? dtm : 0.0f;
+}
+
+// Suffix sums of (Bqp' w): given err/w in S.err[13*i + s] (rows 0..11),
+// write W0[13*j + s] = sum_{i>=j} w_i[s], W1 = sum_{i>=j} (i-j) w_i[s].
+template <int W>
+__device__ __forceinline__ void suffix_sums(SrbdLds<W> &S, int N) {
+  const int t = threadIdx.x;
+  if (t < 12) {
+    float a0 = 0.0f, a1 = 0.0f;
+    for (int i = N - 1; i >= 0; --i) {
+      a1 += a0;
+      a0 += S.err[13 * i + t];
+      S.W0[13 * i + t] = a0;
+      S.W1[13 * i + t] = a1;
+    }
+  }
+}
+
+// (Bqp' w)_v for this lane's variable from W0/W1 of its step.
+__device__ __forceinline__ float bqp_t_w(const float *W0, const float *W1, int step,
+                                         const f8v bvr, float dtm, float dt2m) {
+  const int comp = (int)bvr[7];
+  const float *w0 = W0 + 13 * step, *w1 = W1 + 13 * step;
+  float acc = bvr[0] * w0[6] + bvr[1] * w0[7] + bvr[2] * w0[8];
+  acc += dtm * w0[9 + comp];
+  acc += bvr[3] * w1[0] + bvr[4] * w1[1] + bvr[5] * w1[2];
+  acc += dt2m * w1[3 + comp];
+  return acc;
+}
+
+// Unscaled P x (P = Bqp' Q Bqp + R) for this lane's variable.  S.xs holds
+// the unscaled x of every variable.  Four barriers.
+template <int W>
+__device__ __forceinline__ float p_times_x(SrbdLds<W> &S, const SrbdArgs &a, int N, int nvalid, bool valid,
+                           int step, const f8v bvr, float r2v, float xv, float dtm,
+                           float dt2m) {
+  const int t = threadIdx.x;
+  // (a) per-step aggregates agg_j[s] = sum_{v in step j} coef(v, s) x_v
+  for (int idx = t; idx < 12 * N; idx += 64 * W) {
+    const int j = idx / 12, s = idx - 12 * j;
+    float acc = 0.0f;
+    for (int p = S.stepstart[j]; p < S.stepstart[j + 1]; ++p) {
+      const int vb = 64 * (p / kLegsPerWave) + 3 * (p % kLegsPerWave);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) acc += coef_row(S.bv[vb + c], s, dtm, dt2m) * S.xs[vb + c];
+    }
+    S.agg[idx] = acc;
+  }
+  __syncthreads();
+  // (b) state trajectory s_i = sum_{j<=i} [B rows: agg_j ; E rows: (i-j) agg_j],
+  //     w_i = Q s_i, then suffix sums (same lane owns one row s throughout)
+  if (t < 12) {
+    float pa = 0.0f, pe = 0.0f, s1 = 0.0f;
+    const bool brow = t >= 6;
+    for (int i = 0; i < N; ++i) {
+      const float ag = S.agg[12 * i + t];
+      s1 += pe;  // sum_{j<i} agg_j accumulated (i-j) times
+      pe += ag;
+      pa += ag;
+      const float si = brow ? pa : s1;
+      S.err[13 * i + t] = a.q2[t] * si;
+    }
+  }
+  suffix_sums<W>(S, N);
+  __syncthreads();
+  float px = 0.0f;
+  if (valid) px = bqp_t_w(S.W0, S.W1, step, bvr, dtm, dt2m) + r2v * xv;
+  __syncthreads();
+  (void)nvalid;
+  return px;
+}
+
+// Per-lane state of one stance variable and its owned constraint rows.
+struct LaneVar {
+  int t, lane, comp, step, leg, nrow, zl;
+  bool valid;
+  f8v bvr;
+  float r2v, bq0, bq1, bq2, eq0, eq1, eq2, linb, line;
+  f2v ra, rz, rl, ru, rE, Einv, lh, uh, rv;
+  i2v ctype;
+  float Dr, Dinv, cs, cinv, qv;
+  float x;
+  f2v zr, yr;
+};
+
+template <int W>
+struct ColMask {
+  int wcols[W];
+  __device__ __forceinline__ bool ok(int c0) const { return (c0 & 63) < wcols[c0 >> 6]; }
+};
+
+// Unscaled condensed-Hessian row (closed form), identity on padding lanes.
+template <int W>
+__device__ __forceinline__ void gen_p_row(const SrbdLds<W> &S, const LaneVar &v, int N,
+                                          const ColMask<W> &cm, Row<W> &K) {
+  constexpr int NC = 64 * W;
+  // opaque copies: keep LICM from hoisting 64 per-column masks / LDS loads
+  // out of the ADMM loop (that would blow the VGPR budget)
+  int tt = v.t, st = v.step, cp = v.comp;
+  asm volatile("" : "+v"(tt), "+v"(st), "+v"(cp)::"memory");
+  K.zero();
+#pragma unroll
+  for (int c0 = 0; c0 < NC; c0 += 4) {
+    if (!cm.ok(c0)) continue;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int c = c0 + cc;
+      const float4 lo = *reinterpret_cast<const float4 *>(&S.bv[c][0]);
+      const float4 hi = *reinterpret_cast<const float4 *>(&S.bv[c][4]);
+      float K0, K2;
+      k0k2(st, (int)hi.z, N, K0, K2);
+      const bool same = (cp == (int)hi.w);
+      const float beta = v.bq0 * lo.x + v.bq1 * lo.y + v.bq2 * lo.z + (same ? v.linb : 0.0f);
+      const float epsv = v.eq0 * lo.w + v.eq1 * hi.x + v.eq2 * hi.y + (same ? v.line : 0.0f);
+      float pv = K0 * beta + K2 * epsv;
+      pv += (c == tt) ? v.r2v : 0.0f;
+      K.set(c, v.valid ? pv : 0.0f);
+    }
+  }
+}
+
+// P <- cs * D P D with the final Ruiz scaling (D of every column in bc[0]).
+template <int W>
+__device__ __forceinline__ void scale_p_row(SrbdLds<W> &S, const LaneVar &v,
+                                            const ColMask<W> &cm, Row<W> &K) {
+  constexpr int NC = 64 * W;
+  S.bc[0][v.t] = v.Dr;
+  __syncthreads();
+  const float sr = v.cs * v.Dr;
+#pragma unroll
+  for (int c0 = 0; c0 < NC; c0 += 4) {
+    if (!cm.ok(c0)) continue;
+    const float4 d4 = *reinterpret_cast<const float4 *>(&S.bc[0][c0]);
+    K.set(c0 + 0, K.get(c0 + 0) * (sr * d4.x));
+    K.set(c0 + 1, K.get(c0 + 1) * (sr * d4.y));
+    K.set(c0 + 2, K.get(c0 + 2) * (sr * d4.z));
+    K.set(c0 + 3, K.get(c0 + 3) * (sr * d4.w));
+  }
+  __syncthreads();
+}
+
+// K += sigma I + A' diag(rho) A  (leg-local 3x3 block)
+template <int W>
+__device__ __forceinline__ void add_leg_block(const LaneVar &v, float sigma,
+                                              const ColMask<W> &cm, Row<W> &K) {
+  constexpr int NC = 64 * W;
+  const float d_own = v.rv[0] * v.ra[0] * v.ra[0] + v.rv[1] * v.ra[1] * v.ra[1];
+  const float d_oz = v.rv[0] * v.ra[0] * v.rz[0] + v.rv[1] * v.ra[1] * v.rz[1];
+  const float d_zz = v.rv[0] * v.rz[0] * v.rz[0] + v.rv[1] * v.rz[1] * v.rz[1];
+  const int l1 = (v.lane + 63) & 63, l2 = (v.lane + 62) & 63;
+  const float oz1 = __shfl(d_oz, l1, 64), oz2 = __shfl(d_oz, l2, 64);
+  const float zz1 = __shfl(d_zz, l1, 64), zz2 = __shfl(d_zz, l2, 64);
+  float add0, add1, add2;
+  if (v.comp == 0) {
+    add0 = d_own + sigma; add1 = 0.0f; add2 = d_oz;
+  } else if (v.comp == 1) {
+    add0 = 0.0f; add1 = d_own + sigma; add2 = d_oz;
+  } else {
+    add0 = oz2; add1 = oz1; add2 = d_own + zz1 + zz2 + sigma;
+  }
+  if (!v.valid) { add0 = add1 = add2 = 0.0f; }
+  int c_base = v.t - v.comp;
+  asm volatile("" : "+v"(c_base)::"memory");
+#pragma unroll
+  for (int c0 = 0; c0 < NC; c0 += 4) {
+    if (!cm.ok(c0)) continue;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int c = c0 + cc;
+      const int off = c - c_base;
+      float a = (off == 0) ? add0 : 0.0f;
+      a = (off == 1) ? add1 : a;
+      a = (off == 2) ? add2 : a;
+      K.set(c, K.get(c) + (a));
+    }
+  }
+}
+
+// In-place Gauss-Jordan inverse of the register-resident SPD K (no
+// pivoting; Ruiz-scaled, so pivots are O(1)).  Row k is broadcast through
+// LDS with entry k replaced by p+1 and p in a side slot.  With
+// g = A_rk / p (g = 1 - 1/p on the pivot lane) ONE shared update
+//   A_rc <- A_rc - g * bcast_c
+// performs the whole GJ step, column k included (non-pivot:
+// A_rk - g(p+1) = -g; pivot: p - (1-1/p)(p+1) = 1/p).  A_rk itself is read
+// from the broadcast row: GJ on a symmetric matrix keeps
+// A_rk = +A_kr for unprocessed r and -A_kr for processed r (< k).  No
+// register is ever indexed dynamically, so the row stays in VGPRs.
+template <int W>
+__device__ __forceinline__ void invert(SrbdLds<W> &S, int t, const ColMask<W> &cm,
+                                       Row<W> &K) {
+  constexpr int NC = 64 * W;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    for (int kk = 0; kk < cm.wcols[w]; ++kk) {
+      const int k = 64 * w + kk;
+      const int buf = kk & 1;
+      const bool mine = (t == k);
+      if (mine) {
+#pragma unroll
+        for (int c0 = 0; c0 < NC; c0 += 4) {
+          if (!cm.ok(c0)) continue;
+          float4 v4;
+          v4.x = K.get(c0 + 0);
+          v4.y = K.get(c0 + 1);
+          v4.z = K.get(c0 + 2);
+          v4.w = K.get(c0 + 3);
+          *reinterpret_cast<float4 *>(&S.bc[buf][c0]) = v4;
+        }
+        const float p = S.bc[buf][k];
+        S.piv[buf] = p;
+        S.bc[buf][k] = p + 1.0f;
+      }
+      __syncthreads();
+      const float p = S.piv[buf];
+      const float pinv = 1.0f / p;
+      const float akr = S.bc[buf][t];
+      const float ak = (t < k) ? -akr : akr;
+      const float g = mine ? (1.0f - pinv) : ak * pinv;
+#pragma unroll
+      for (int c0 = 0; c0 < NC; c0 += 4) {
+        if (!cm.ok(c0)) continue;
+        const float4 p4 = *reinterpret_cast<const float4 *>(&S.bc[buf][c0]);
+        K.set(c0 + 0, fmaf(-g, p4.x, K.get(c0 + 0)));
+        K.set(c0 + 1, fmaf(-g, p4.y, K.get(c0 + 1)));
+        K.set(c0 + 2, fmaf(-g, p4.z, K.get(c0 + 2)));
+        K.set(c0 + 3, fmaf(-g, p4.w, K.get(c0 + 3)));
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// OSQP update_info: residual norms (all threads participate).
+//  o[0] ||E^-1(Ax-z)||  o[1] ||E^-1 z||  o[2] ||E^-1 A x||  o[3] ||D^-1 rd||
+//  o[4] ||D^-1 q||  o[5] ||D^-1 A'y||  o[6] ||D^-1 P x||  o[7..13] scaled
+//  versions of (Ax-z, z, Ax, rd, q, A'y, Px) for the rho estimate.
+template <int W>
+__device__ __forceinline__ void residuals(SrbdLds<W> &S, const SrbdArgs &a, const LaneVar &v,
+                                          int N, float dtm, float dt2m, float (&o)[14],
+                                          float &px_out) {
+  S.xs[v.t] = v.valid ? v.x * v.Dr : 0.0f;
+  __syncthreads();
+  const float pxo = p_times_x<W>(S, a, N, 0, v.valid, v.step, v.bvr, v.r2v, S.xs[v.t], dtm, dt2m);
+  const float pxh = v.cs * v.Dr * pxo;
+  px_out = pxh;
+  const float xz = __shfl(v.x, v.zl & 63, 64);
+  const float ay_own = v.ra[0] * v.yr[0] + v.ra[1] * v.yr[1];
+  const float ay_z = v.rz[0] * v.yr[0] + v.rz[1] * v.yr[1];
+  const float a1 = __shfl(ay_z, (v.lane + 63) & 63, 64), a2 = __shfl(ay_z, (v.lane + 62) & 63, 64);
+  const float aty = v.valid ? (ay_own + (v.comp == 2 ? (a1 + a2) : 0.0f)) : 0.0f;
+  const float rd = v.valid ? (v.qv + pxh + aty) : 0.0f;
+  float ax[2], rp[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    ax[k] = (k < v.nrow) ? v.ra[k] * v.x + v.rz[k] * xz : 0.0f;
+    rp[k] = (k < v.nrow) ? ax[k] - v.zr[k] : 0.0f;
+  }
+  o[0] = fmaxf(fabsf(v.Einv[0] * rp[0]), fabsf(v.Einv[1] * rp[1]));
+  o[1] = fmaxf(fabsf(v.Einv[0] * v.zr[0]), fabsf(v.Einv[1] * v.zr[1]));
+  o[2] = fmaxf(fabsf(v.Einv[0] * ax[0]), fabsf(v.Einv[1] * ax[1]));
+  o[3] = fabsf(v.Dinv * rd);
+  o[4] = fabsf(v.Dinv * v.qv);
+  o[5] = fabsf(v.Dinv * aty);
+  o[6] = fabsf(v.Dinv * pxh);
+  o[7] = fmaxf(fabsf(rp[0]), fabsf(rp[1]));
+  o[8] = fmaxf(fabsf(v.zr[0]), fabsf(v.zr[1]));
+  o[9] = fmaxf(fabsf(ax[0]), fabsf(ax[1]));
+  o[10] = fabsf(rd);
+  o[11] = fabsf(v.qv);
+  o[12] = fabsf(aty);
+  o[13] = fabsf(pxh);
+  const bool is_sum[14] = {false, false, false, false, false, false, false,
+                           false, false, false, false, false, false, false};
+  block_reduce<W, 14>(o, is_sum, S.red);
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ? 2 : 1))) void srbd_admm_kernel(const SrbdArgs a) {
+  constexpr int NC = 64 * W;
+  __shared__ __attribute__((aligned(16))) SrbdLds<W> S;
+  const int t = threadIdx.x;
+  const int wave = t >> 6, lane = t & 63;
+  const int64_t b = blockIdx.x;
+  if (b >= a.batch) return;
+  const int N = a.N;
+  const float dt = a.dt, m = a.mass;
+  const float dtm = dt / m, dt2m = dt * dt / m;
+
+  // ---------------- 1. inputs -> LDS (one instance per block)
+  for (int k = t; k < 13; k += NC) S.x0[k] = a.x0[b * 13 + k];
+  {
+    const int nct = a.contacts_per_step ? 4 * N : 4;
+    for (int k = t; k < 4 * N; k += NC)
+      S.ct[k] = a.contacts[b * nct + (a.contacts_per_step ? k : (k & 3))] ? 1 : 0;
+  }
+  __syncthreads();
+
+  // ---------------- 2. stance enumeration (integer, bit-exact)
+  if (wave == 0) {
+    int base = 0;
+    for (int p0 = 0; p0 < 4 * N; p0 += 64) {
+      const int p = p0 + lane;
+      const bool st = (p < 4 * N) && S.ct[p];
+      const uint64_t msk = __ballot(st);
+      const int idx = base + __popcll(msk & ((1ull << lane) - 1ull));
+      if (st) S.legtab[idx] = p;
+      base += __popcll(msk);
+    }
+    if (lane == 0) S.nlegs = base;
+    for (int j = lane; j <= N; j += 64) {
+      int c = 0;
+      for (int p = 0; p < 4 * j; ++p) c += S.ct[p];
+      S.stepstart[j] = c;
+    }
+  }
+  __syncthreads();
+  const int nlegs = uni(S.nlegs);
+  const int n = 3 * nlegs;
+  if (nlegs > kLegsPerWave * W) {  // uniform: host picks W from the batch max
+    if (t < 12) a.u0[b * 12 + t] = NAN;
+    if (t == 0 && a.status) a.status[b] = QLOCO_BAD_SIZE;
+    return;
+  }
+  LaneVar v;
+  v.t = t;
+  v.lane = lane;
+  {
+    const int lslot = lane / 3;
+    v.comp = lane - 3 * lslot;
+    const int L = kLegsPerWave * wave + lslot;
+    v.valid = (lane < 63) && (L < nlegs);
+    const int pair = v.valid ? S.legtab[L] : 0;
+    v.step = pair >> 2;
+    v.leg = pair & 3;
+    v.zl = (v.comp == 2) ? lane : (lane + 2 - v.comp);
+  }
+  ColMask<W> cm;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    int lw = nlegs - kLegsPerWave * w;
+    lw = lw < 0 ? 0 : (lw > kLegsPerWave ? kLegsPerWave : lw);
+    cm.wcols[w] = 3 * lw;
+  }
+
+  // ---------------- 3. SRBD model terms (ConvexMpc.cpp:111-160, compute_grf :502-549)
+  const float yaw = S.x0[2];
+  const float cy = cosf(yaw), sy = sinf(yaw);
+  // R = [[c,s,0],[-s,c,0],[0,0,1]] (A1RobotControl.cpp:506-508)
+  const float R00 = cy, R01 = sy, R10 = -sy, R11 = cy;
+  float Ii[3][3];
+  {
+    const float *I = a.inertia;
+    const float Rm[3][3] = {{R00, R01, 0.f}, {R10, R11, 0.f}, {0.f, 0.f, 1.f}};
+    float RI[3][3], Iw[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        RI[r][c] = Rm[r][0] * I[c * 3 + 0] + Rm[r][1] * I[c * 3 + 1] + Rm[r][2] * I[c * 3 + 2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        Iw[r][c] = RI[r][0] * Rm[c][0] + RI[r][1] * Rm[c][1] + RI[r][2] * Rm[c][2];
+    const float c00 = Iw[1][1] * Iw[2][2] - Iw[1][2] * Iw[2][1];
+    const float c01 = Iw[1][2] * Iw[2][0] - Iw[1][0] * Iw[2][2];
+    const float c02 = Iw[1][0] * Iw[2][1] - Iw[1][1] * Iw[2][0];
+    const float id = 1.0f / (Iw[0][0] * c00 + Iw[0][1] * c01 + Iw[0][2] * c02);
+    Ii[0][0] = c00 * id;
+    Ii[1][0] = c01 * id;
+    Ii[2][0] = c02 * id;
+    Ii[0][1] = (Iw[0][2] * Iw[2][1] - Iw[0][1] * Iw[2][2]) * id;
+    Ii[1][1] = (Iw[0][0] * Iw[2][2] - Iw[0][2] * Iw[2][0]) * id;
+    Ii[2][1] = (Iw[0][1] * Iw[2][0] - Iw[0][0] * Iw[2][1]) * id;
+    Ii[0][2] = (Iw[0][1] * Iw[1][2] - Iw[0][2] * Iw[1][1]) * id;
+    Ii[1][2] = (Iw[0][2] * Iw[1][0] - Iw[0][0] * Iw[1][2]) * id;
+    Ii[2][2] = (Iw[0][0] * Iw[1][1] - Iw[0][1] * Iw[1][0]) * id;
+  }
+  // this lane's B_d column (rows 6..8) and E = dt A_c B_d column (rows 0..2)
+  {
+    const float *rf = a.feet + b * (a.feet_per_step ? 12 * N : 12) +
+                      (a.feet_per_step ? 12 * v.step : 0) + 3 * v.leg;
+    const float rx = rf[0], ry = rf[1], rz = rf[2];
+    const int comp = v.comp;
+    float tv0 = comp == 0 ? 0.f : (comp == 1 ? -rz : ry);  // skew(r) e_comp (Utils.cpp:35-41)
+    float tv1 = comp == 0 ? rz : (comp == 1 ? 0.f : -rx);
+    float tv2 = comp == 0 ? -ry : (comp == 1 ? rx : 0.f);
+    float ba[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) ba[r] = dt * (Ii[r][0] * tv0 + Ii[r][1] * tv1 + Ii[r][2] * tv2);
+    v.bvr[0] = ba[0];
+    v.bvr[1] = ba[1];
+    v.bvr[2] = ba[2];
+    v.bvr[3] = dt * (R00 * ba[0] + R01 * ba[1]);
+    v.bvr[4] = dt * (R10 * ba[0] + R11 * ba[1]);
+    v.bvr[5] = dt * ba[2];
+    v.bvr[6] = (float)v.step;
+    v.bvr[7] = v.valid ? (float)comp : -1.0f;
+    if (!v.valid) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) v.bvr[k] = 0.0f;
+    }
+    *reinterpret_cast<float4 *>(&S.bv[t][0]) = make_float4(v.bvr[0], v.bvr[1], v.bvr[2], v.bvr[3]);
+    *reinterpret_cast<float4 *>(&S.bv[t][4]) = make_float4(v.bvr[4], v.bvr[5], v.bvr[6], v.bvr[7]);
+  }
+  v.r2v = v.valid ? a.r2[3 * v.leg + v.comp] : 0.0f;
+  v.bq0 = a.q2[6] * v.bvr[0];
+  v.bq1 = a.q2[7] * v.bvr[1];
+  v.bq2 = a.q2[8] * v.bvr[2];
+  v.eq0 = a.q2[0] * v.bvr[3];
+  v.eq1 = a.q2[1] * v.bvr[4];
+  v.eq2 = a.q2[2] * v.bvr[5];
+  v.linb = v.valid ? a.q2[9 + v.comp] * dtm * dtm : 0.0f;
+  v.line = v.valid ? a.q2[3 + v.comp] * dt2m * dt2m : 0.0f;
+
+  // ---------------- 4. gradient g = Bqp' Q (Aqp x0 - x_ref) (ConvexMpc.cpp:219-221)
+  //     free response A_d^{i+1} x0 in closed form (A_c nilpotent)
+  for (int idx = t; idx < 13 * N; idx += NC) {
+    const int i = idx / 13, s = idx - 13 * i;
+    const float k = (float)(i + 1);
+    const float *x0 = S.x0;
+    float xf;
+    if (s < 3) {
+      const float rw = s == 0 ? (R00 * x0[6] + R01 * x0[7]) : (s == 1 ? (R10 * x0[6] + R11 * x0[7]) : x0[8]);
+      xf = x0[s] + k * dt * rw;
+    } else if (s < 6) {
+      xf = x0[s] + k * dt * x0[s + 6];
+      if (s == 5) xf += 0.5f * k * (k - 1.0f) * dt * dt * x0[12];
+    } else if (s < 9) {
+      xf = x0[s];
+    } else if (s < 12) {
+      xf = x0[s] + (s == 11 ? k * dt * x0[12] : 0.0f);
+    } else {
+      xf = x0[12];
+    }
+    S.err[idx] = a.q2[s] * (xf - a.xref[b * 13 * N + idx]);
+  }
+  __syncthreads();
+  suffix_sums<W>(S, N);
+  __syncthreads();
+  v.qv = v.valid ? bqp_t_w(S.W0, S.W1, v.step, v.bvr, dtm, dt2m) : 0.0f;
+
+  // ---------------- 5. P row in registers (unscaled)
+  Row<W> K;
+  gen_p_row<W>(S, v, N, cm, K);
+
+  // ---------------- 6. constraint rows owned by this lane (ConvexMpc.cpp:47-59, :227-249)
+  //  x lane: rows 0 [1,0, mu] in [0,inf), 1 [1,0,-mu] in (-inf,0]
+  //  y lane: rows 2 [0,1, mu] in [0,inf), 3 [0,1,-mu] in (-inf,0]
+  //  z lane: row 4 [0,0,1] in [fz_min, fz_max]
+  v.nrow = v.valid ? (v.comp == 2 ? 1 : 2) : 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const bool rvld = k < v.nrow;
+    v.ra[k] = rvld ? 1.0f : 0.0f;
+    v.rz[k] = (rvld && v.comp < 2) ? (k == 0 ? a.mu : -a.mu) : 0.0f;
+    if (v.comp < 2) {
+      v.rl[k] = k == 0 ? 0.0f : -INFINITY;
+      v.ru[k] = k == 0 ? INFINITY : 0.0f;
+    } else {
+      v.rl[k] = a.fz_min;
+      v.ru[k] = a.fz_max;
+    }
+    v.rE[k] = 1.0f;
+  }
+  v.Dr = 1.0f;
+  v.cs = 1.0f;
+
+  // ---------------- 7. modified Ruiz equilibration (OSQP scaling.c)
+  for (int it = 0; it < a.scaling; ++it) {
+    float cnP = 0.0f;
+#pragma unroll
+    for (int c0 = 0; c0 < NC; c0 += 4) {
+      if (!cm.ok(c0)) continue;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) cnP = fmaxf(cnP, fabsf(K.get(c0 + cc)));
+    }
+    float cnA = fmaxf(fabsf(v.ra[0]), fabsf(v.ra[1]));
+    const float zmax_own = fmaxf(fabsf(v.rz[0]), fabsf(v.rz[1]));
+    const float zm1 = __shfl(zmax_own, (lane + 63) & 63, 64);
+    const float zm2 = __shfl(zmax_own, (lane + 62) & 63, 64);
+    if (v.comp == 2) cnA = fmaxf(cnA, fmaxf(zm1, zm2));
+    const float Dt = v.valid ? 1.0f / sqrtf(limit_scaling(fmaxf(cnP, cnA))) : 1.0f;
+    float Et[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      Et[k] = (k < v.nrow) ? 1.0f / sqrtf(limit_scaling(fmaxf(fabsf(v.ra[k]), fabsf(v.rz[k])))) : 1.0f;
+    const int buf = it & 1;
+    S.bc[buf][t] = Dt;
+    __syncthreads();
+    float cn2 = 0.0f;
+#pragma unroll
+    for (int c0 = 0; c0 < NC; c0 += 4) {
+      if (!cm.ok(c0)) continue;
+      const float4 d4 = *reinterpret_cast<const float4 *>(&S.bc[buf][c0]);
+      const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const int c = c0 + cc;
+        K.set(c, K.get(c) * (Dt * dd[cc]));
+        cn2 = fmaxf(cn2, fabsf(K.get(c)));
+      }
+    }
+    const float Dz = S.bc[buf][v.zl + 64 * wave];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      v.ra[k] *= Et[k] * Dt;
+      v.rz[k] *= Et[k] * Dz;
+      v.rE[k] *= Et[k];
+    }
+    v.qv *= Dt;
+    v.Dr *= Dt;
+    // cost scaling: mean column norm of P vs ||q||_inf
+    float rv2[2] = {v.valid ? cn2 : 0.0f, v.valid ? fabsf(v.qv) : 0.0f};
+    const bool is_sum2[2] = {true, false};
+    block_reduce<W, 2>(rv2, is_sum2, S.red);
+    const float meanP = rv2[0] / (float)(n > 0 ? n : 1);
+    const float qn = limit_scaling(rv2[1]);
+    const float ct = 1.0f / limit_scaling(fmaxf(meanP, qn));
+    K.scale(ct);
+    v.qv *= ct;
+    v.cs *= ct;
+  }
+  v.cinv = 1.0f / v.cs;
+  v.Dinv = 1.0f / v.Dr;
+  float rho = fminf(fmaxf(a.rho, 1e-6f), 1e6f);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    v.Einv[k] = 1.0f / v.rE[k];
+    v.lh[k] = v.rl[k] * v.rE[k];
+    v.uh[k] = v.ru[k] * v.rE[k];
+    // OSQP set_rho_vec: loose / equality / inequality rows
+    if (v.lh[k] < -1e26f && v.uh[k] > 1e26f) v.ctype[k] = -1;
+    else if (v.uh[k] - v.lh[k] < 1e-4f) v.ctype[k] = 1;
+    else v.ctype[k] = 0;
+    v.rv[k] = v.ctype[k] == -1 ? 1e-6f : (v.ctype[k] == 1 ? 1e3f * rho : rho);
+    if (k >= v.nrow) v.rv[k] = 1.0f;  // unused slot (avoid 0-division)
+  }
+  __syncthreads();
+
+  // ---------------- 8. K = P + sigma I + A' rho A, inverse in registers
+  add_leg_block<W>(v, a.sigma, cm, K);
+  invert<W>(S, t, cm, K);
+  int rho_updates = 0;
+
+  // ---------------- 9. ADMM iterations (OSQP osqp_solve)
+  v.x = 0.0f;
+  v.zr[0] = v.zr[1] = 0.0f;
+  v.yr[0] = v.yr[1] = 0.0f;
+  if (a.warm_start) {
+    const int nu = 12 * N, ncn = 20 * N;
+    const float *wx = a.warm + b * (nu + ncn);
+    const float *wy = wx + nu;
+    v.x = v.valid ? wx[12 * v.step + 3 * v.leg + v.comp] * v.Dinv : 0.0f;
+    const int rbase = 20 * v.step + 5 * v.leg + (v.comp == 0 ? 0 : (v.comp == 1 ? 2 : 4));
+#pragma unroll
+    for (int k = 0; k < 2; ++k) v.yr[k] = (k < v.nrow) ? wy[rbase + k] * v.Einv[k] * v.cs : 0.0f;
+    const float xz = __shfl(v.x, v.zl & 63, 64);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) v.zr[k] = (k < v.nrow) ? v.ra[k] * v.x + v.rz[k] * xz : 0.0f;
+  }
+  const float alpha = a.alpha, sigma = a.sigma;
+  const int interval = (a.adaptive_rho && a.rho_interval == 0)
+                           ? (a.check_termination ? 4 * a.check_termination : 100)
+                           : a.rho_interval;
+  int status = QLOCO_MAX_ITER, iter;
+  float px_last = 0.0f;
+  bool can_check = false;
+  const int l1 = (lane + 63) & 63, l2 = (lane + 62) & 63;
+
+  for (iter = 1; iter <= a.max_iter; ++iter) {
+    const float xp = v.x;
+    const float zp0 = v.zr[0], zp1 = v.zr[1];
+    // rhs = sigma x_prev - q + A'(rho z_prev - y)   (compute_rhs)
+    const float w0 = v.rv[0] * zp0 - v.yr[0], w1 = v.rv[1] * zp1 - v.yr[1];
+    const float own = v.ra[0] * w0 + v.ra[1] * w1;
+    const float tz = v.rz[0] * w0 + v.rz[1] * w1;
+    const float t1 = __shfl(tz, l1, 64), t2 = __shfl(tz, l2, 64);
+    const float rhs = v.valid ? (sigma * xp - v.qv + own + (v.comp == 2 ? (t1 + t2) : 0.0f)) : 0.0f;
+    const int buf = iter & 1;
+    S.bc[buf][t] = rhs;
+    __syncthreads();
+    // x_tilde = K^-1 rhs  (register-resident matvec)
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+#pragma unroll
+    for (int c0 = 0; c0 < NC; c0 += 4) {
+      if (!cm.ok(c0)) continue;
+      const float4 r4 = *reinterpret_cast<const float4 *>(&S.bc[buf][c0]);
+      acc0 = fmaf(K.get(c0 + 0), r4.x, acc0);
+      acc1 = fmaf(K.get(c0 + 1), r4.y, acc1);
+      acc2 = fmaf(K.get(c0 + 2), r4.z, acc2);
+      acc3 = fmaf(K.get(c0 + 3), r4.w, acc3);
+    }
+    const float xt = v.valid ? ((acc0 + acc1) + (acc2 + acc3)) : 0.0f;
+    const float xtz = __shfl(xt, v.zl & 63, 64);
+    // update_x / update_z / update_y
+    v.x = alpha * xt + (1.0f - alpha) * xp;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k < v.nrow) {
+        const float zt = v.ra[k] * xt + v.rz[k] * xtz;
+        const float zrel = alpha * zt + (1.0f - alpha) * (k == 0 ? zp0 : zp1);
+        const float vv = zrel + v.yr[k] / v.rv[k];
+        const float zn = fminf(fmaxf(vv, v.lh[k]), v.uh[k]);
+        v.yr[k] += v.rv[k] * (zrel - zn);
+        v.zr[k] = zn;
+      }
+    }
+    can_check = a.check_termination && (iter % a.check_termination == 0);
+    const bool do_rho = a.adaptive_rho && interval && (iter % interval == 0);
+    if (can_check || do_rho) {
+      float o[14];
+      residuals<W>(S, a, v, N, dtm, dt2m, o, px_last);
+      const float pri_res = o[0], dua_res = v.cinv * o[3];
+      if (can_check) {
+        const float eps_p = a.eps_abs + a.eps_rel * fmaxf(o[1], o[2]);
+        const float eps_d = a.eps_abs + a.eps_rel * v.cinv * fmaxf(fmaxf(o[4], o[5]), o[6]);
+        if (pri_res < eps_p && dua_res < eps_d) {
+          status = QLOCO_OK;
+          break;
+        }
+      }
+      if (do_rho) {  // compute_rho_estimate + adapt_rho
+        const float pn = o[7] / (fmaxf(o[8], o[9]) + 1e-30f);
+        const float dn = o[10] / (fmaxf(fmaxf(o[11], o[12]), o[13]) + 1e-30f);
+        float rho_new = rho * sqrtf(pn / (dn + 1e-30f));
+        rho_new = fminf(fmaxf(rho_new, 1e-6f), 1e6f);
+        if (rho_new > rho * a.rho_tol || rho_new < rho / a.rho_tol) {
+          rho = rho_new;
+#pragma unroll
+          for (int k = 0; k < 2; ++k)
+            if (k < v.nrow) v.rv[k] = v.ctype[k] == 0 ? rho : (v.ctype[k] == 1 ? 1e3f * rho : 1e-6f);
+          gen_p_row<W>(S, v, N, cm, K);
+          scale_p_row<W>(S, v, cm, K);
+          add_leg_block<W>(v, sigma, cm, K);
+          invert<W>(S, t, cm, K);
+          rho_updates++;
+        }
+      }
+    }
+  }
+  bool have_px = (status == QLOCO_OK);
+  if (iter > a.max_iter) {
+    iter = a.max_iter;
+    float o[14];
+    residuals<W>(S, a, v, N, dtm, dt2m, o, px_last);
+    have_px = true;
+    const float pri_res = o[0], dua_res = v.cinv * o[3];
+    const float ep = 10.f * a.eps_abs + 10.f * a.eps_rel * fmaxf(o[1], o[2]);
+    const float ed = 10.f * a.eps_abs + 10.f * a.eps_rel * v.cinv * fmaxf(fmaxf(o[4], o[5]), o[6]);
+    status = (pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE : QLOCO_MAX_ITER;
+  }
+
+  // ---------------- 10. outputs: unscale, objective, scatter to leg slots
+  if (!have_px) {
+    float o[14];
+    residuals<W>(S, a, v, N, dtm, dt2m, o, px_last);
+  }
+  const float xu = v.valid ? v.x * v.Dr : 0.0f;
+  float objp[1] = {v.valid ? v.cinv * (0.5f * v.x * px_last + v.qv * v.x) : 0.0f};
+  {
+    const bool is_sum1[1] = {true};
+    block_reduce<W, 1>(objp, is_sum1, S.red);
+  }
+  const bool bad = !isfinite(objp[0]);
+  if (bad) status = QLOCO_NAN;
+  if (a.u) {  // full solution (world frame), swing forces exactly 0
+    float *uo = a.u + b * 12 * N;
+    for (int k = t; k < 12 * N; k += NC) uo[k] = 0.0f;
+    __syncthreads();
+    if (v.valid) uo[12 * v.step + 3 * v.leg + v.comp] = bad ? NAN : xu;
+  }
+  // u0: step-0 forces; optional body frame R' u (A1RobotControl.cpp:596-599)
+  S.xs[t] = xu;
+  __syncthreads();
+  if (t < 12) {
+    const int lg = t / 3, cp = t - 3 * lg;
+    float f0 = 0.f, f1 = 0.f, f2 = 0.f;
+    for (int p = 0; p < S.stepstart[1]; ++p) {
+      if ((S.legtab[p] & 3) == lg) {
+        const int vb = 64 * (p / kLegsPerWave) + 3 * (p % kLegsPerWave);
+        f0 = S.xs[vb];
+        f1 = S.xs[vb + 1];
+        f2 = S.xs[vb + 2];
+      }
+    }
+    float o = cp == 0 ? f0 : (cp == 1 ? f1 : f2);
+    if (a.output_frame == 1)  // R^T f with R = [[c,s,0],[-s,c,0],[0,0,1]]
+      o = cp == 0 ? (R00 * f0 + R10 * f1) : (cp == 1 ? (R01 * f0 + R11 * f1) : f2);
+    a.u0[b * 12 + t] = bad ? NAN : o;
+  }
+  if (a.warm_start) {
+    const int nu = 12 * N, ncn = 20 * N;
+    float *wx = a.warm + b * (nu + ncn);
+    float *wy = wx + nu;
+    for (int k = t; k < nu + ncn; k += NC) wx[k] = 0.0f;
+    __syncthreads();
+    if (v.valid) {
+      wx[12 * v.step + 3 * v.leg + v.comp] = xu;
+      const int rbase = 20 * v.step + 5 * v.leg + (v.comp == 0 ? 0 : (v.comp == 1 ? 2 : 4));
+      for (int k = 0; k < v.nrow; ++k) wy[rbase + k] = v.cinv * v.rE[k] * v.yr[k];
+    }
+  }
+  if (t == 0) {
+    if (a.status) a.status[b] = status;
+    if (a.iters) a.iters[b] = iter;
+    if (a.rho_updates) a.rho_updates[b] = rho_updates;
+    if (a.obj) a.obj[b] = objp[0];
+  }
+}
+
+}  // namespace qloco
+
+using namespace qloco;
+
+extern "C" void qloco_srbd_spec_default(qloco_srbd_spec *s) {
+  memset(s, 0, sizeof(*s));
+  s->horizon = 10;
+  s->feet_per_step = 0;
+  s->contacts_per_step = 1;
+  s->output_frame = 0;
+  s->dt = 0.0025f;
+  s->mass = 12.0f;  // gait::mass (robot_const_para_config.cpp:32)
+  // Momentum_sum = 2 x Go1 trunk inertia (servo.cpp:375-377, go1.urdf:435)
+  const float I[9] = {2 * 0.0168352186f, 2 * 0.0004636141f, 2 * 0.0002367952f,
+                      2 * 0.0004636141f, 2 * 0.0656071082f, 2 * 3.6671e-05f,
+                      2 * 0.0002367952f, 2 * 3.6671e-05f,   2 * 0.0742720659f};
+  for (int k = 0; k < 9; ++k) s->inertia[k] = I[k];
+  // gazebo_a1_mpc.yaml weights
+  const float q[13] = {20, 10, 1, 0, 0, 420, 0.05f, 0.05f, 0.05f, 30, 30, 10, 0};
+  for (int k = 0; k < 13; ++k) s->q_weights[k] = q[k];
+  for (int k = 0; k < 12; ++k) s->r_weights[k] = 1e-7f;
+  s->mu = 0.3f;
+  s->fz_min = 0.0f;
+  s->fz_max = 180.0f;
+  // OSQP v0.6 defaults
+  s->rho = 0.1f;
+  s->sigma = 1e-6f;
+  s->alpha = 1.6f;
+  s->eps_abs = 1e-3f;
+  s->eps_rel = 1e-3f;
+  s->max_iter = 4000;
+  s->check_termination = 25;
+  s->scaling = 10;
+  s->adaptive_rho = 1;
+  s->adaptive_rho_interval = 0;
+  s->adaptive_rho_tolerance = 5.0f;
+  s->warm_start = 0;
+  s->polish = 0;
+}
+
+extern "C" int qloco_srbd_max_stance_vars(void) { return 3 * kLegsPerWave * 2; }
+
+extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, const float *x0,
+                                   const float *x_ref, const float *feet,
+                                   const uint8_t *contacts, float *u0, float *u,
+                                   int32_t *status, int32_t *iters, int32_t *rho_updates,
+                                   float *obj, float *warm, int32_t max_stance_legs,
+                                   void *stream) {
+  if (!spec || batch < 0 || !x0 || !x_ref || !feet || !contacts || !u0) return QLOCO_ERR_ARG;
+  if (spec->horizon < 1 || spec->horizon > kMaxN) return QLOCO_BAD_SIZE;
+  if (spec->warm_start && !warm) return QLOCO_ERR_ARG;
+  if (batch == 0) return QLOCO_OK;
+  SrbdArgs a;
+  memset(&a, 0, sizeof(a));
+  a.N = spec->horizon;
+  a.feet_per_step = spec->feet_per_step;
+  a.contacts_per_step = spec->contacts_per_step;
+  a.output_frame = spec->output_frame;
+  a.dt = spec->dt;
+  a.mass = spec->mass;
+  for (int k = 0; k < 9; ++k) a.inertia[k] = spec->inertia[k];
+  for (int k = 0; k < 13; ++k) a.q2[k] = 2.0f * spec->q_weights[k];
+  for (int k = 0; k < 12; ++k) a.r2[k] = 2.0f * spec->r_weights[k];
+  a.mu = spec->mu;
+  a.fz_min = spec->fz_min;
+  a.fz_max = spec->fz_max;
+  a.rho = spec->rho;
+  a.sigma = spec->sigma;
+  a.alpha = spec->alpha;
+  a.eps_abs = spec->eps_abs;
+  a.eps_rel = spec->eps_rel;
+  a.max_iter = spec->max_iter;
+  a.check_termination = spec->check_termination;
+  a.scaling = spec->scaling;
+  a.adaptive_rho = spec->adaptive_rho;
+  a.rho_interval = spec->adaptive_rho_interval;
+  a.rho_tol = spec->adaptive_rho_tolerance;
+  a.warm_start = spec->warm_start;
+  a.polish = spec->polish;
+  a.batch = batch;
+  a.x0 = x0;
+  a.xref = x_ref;
+  a.feet = feet;
+  a.contacts = contacts;
+  a.u0 = u0;
+  a.u = u;
+  a.obj = obj;
+  a.warm = warm;
+  a.status = status;
+  a.iters = iters;
+  a.rho_updates = rho_updates;
+  int legs = max_stance_legs > 0 ? max_stance_legs : 4 * spec->horizon;
+  hipStream_t st = (hipStream_t)stream;
+  if (legs <= kLegsPerWave) {
+    hipLaunchKernelGGL(srbd_admm_kernel<1>, dim3((unsigned)batch), dim3(64), 0, st, a);
+  } else if (legs <= 2 * kLegsPerWave) {
+    hipLaunchKernelGGL(srbd_admm_kernel<2>, dim3((unsigned)batch), dim3(128), 0, st, a);
+  } else {
+    return QLOCO_BAD_SIZE;
+  }
+  QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel launch");
+  return QLOCO_OK;
+}
+
+extern "C" int qloco_srbd_solve(const qloco_srbd_spec *spec, int64_t batch, const float *x0,
+                                const float *x_ref, const float *feet, const uint8_t *contacts,
+                                float *u0, float *u, int32_t *status, int32_t *iters, float *obj,
+                                float *warm, void *stream) {
+  return qloco_srbd_solve_ex(spec, batch, x0, x_ref, feet, contacts, u0, u, status, iters,
+                             nullptr, obj, warm, 0, stream);
+}

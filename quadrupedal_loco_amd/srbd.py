@@ -1,0 +1,126 @@
+"""Batched SRBD convex MPC (Go1, N-step horizon, 12 contact forces).
+
+Python mirror of the reference's ConvexMpc + A1RobotControl::compute_grf MPC
+branch (a1_cpp_open_source/src/ConvexMpc.cpp:8-264,
+A1RobotControl.cpp:452-600), batched over independent robot states.  The
+build and the OSQP-algorithm ADMM run in ONE fused gfx950 kernel
+(quadrupedal_loco_amd/csrc/qloco_srbd.hip) behind `qloco_srbd_solve`.
+
+Inputs are device tensors already resident in HBM (torch is only the
+allocator / stream plumbing here):
+  x0        (B, 13)      float32   mpc_states       [rpy, p, omega, v, -9.8]
+  x_ref     (B, 13N)     float32   mpc_states_d
+  feet      (B, 12) or (B, 12N)    foot_pos_abs, legs FL, FR, RL, RR
+  contacts  (B, 4) or (B, 4N)      uint8 contact flags
+"""
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import SrbdSpec, check, lib, ptr
+
+GAITS = {"trot": 0, "pace": 1, "biped": 1, "mixed": 2, "stance": 3}
+
+
+def default_spec(**overrides):
+    """Go1 constants + OSQP default settings."""
+    s = SrbdSpec()
+    lib().qloco_srbd_spec_default(C.byref(s))
+    for k, v in overrides.items():
+        if k in ("inertia", "q_weights", "r_weights"):
+            arr = getattr(s, k)
+            for i, x in enumerate(np.asarray(v, dtype=np.float32).ravel()):
+                arr[i] = float(x)
+        else:
+            setattr(s, k, v)
+    return s
+
+
+def generate(seed, horizon, count, gait="trot", first=0, dt=0.0025):
+    """Deterministic synthetic instances on the host (qloco_gen_srbd_host)."""
+    g = GAITS[gait] if isinstance(gait, str) else int(gait)
+    x0 = np.zeros((count, 13), np.float32)
+    xr = np.zeros((count, 13 * horizon), np.float32)
+    ft = np.zeros((count, 12), np.float32)
+    ct = np.zeros((count, 4 * horizon), np.uint8)
+    check(lib().qloco_gen_srbd_host(seed, horizon, dt, g, first, count, ptr(x0), ptr(xr),
+                                    ptr(ft), ptr(ct)), "qloco_gen_srbd_host")
+    return x0, xr, ft, ct
+
+
+@dataclass
+class SrbdResult:
+    u0: object              # (B, 12) first-step forces
+    u: object = None        # (B, 12N) full solution, world frame
+    status: object = None   # (B,) int32 qloco_status
+    iters: object = None    # (B,) int32 ADMM iterations
+    rho_updates: object = None
+    obj: object = None      # (B,) QP objective 0.5 u'Hu + g'u
+
+
+def max_stance_legs(contacts, horizon, contacts_per_step=True):
+    """Largest number of stance (step, leg) pairs in the batch (host sync)."""
+    if contacts_per_step:
+        return int(contacts.reshape(contacts.shape[0], -1).sum(dim=1).max().item()) \
+            if hasattr(contacts, "sum") and hasattr(contacts, "device") else \
+            int(np.asarray(contacts).reshape(len(contacts), -1).sum(axis=1).max())
+    per = contacts.reshape(contacts.shape[0], 4).sum(dim=1).max().item() \
+        if hasattr(contacts, "device") else np.asarray(contacts).reshape(-1, 4).sum(1).max()
+    return int(per) * horizon
+
+
+class BatchedConvexMpc:
+    """Batched drop-in for ConvexMpc + OsqpEigen::Solver::solve.
+
+    solve() enqueues one kernel on `stream` (default: torch's current
+    stream) and returns device tensors; nothing is synchronised unless
+    `max_legs` has to be computed from the contacts.
+    """
+
+    def __init__(self, spec=None, **overrides):
+        self.spec = spec if spec is not None else default_spec(**overrides)
+
+    @property
+    def horizon(self):
+        return self.spec.horizon
+
+    def alloc_outputs(self, batch, device, full=False, stats=True):
+        import torch
+        N = self.spec.horizon
+        out = SrbdResult(u0=torch.empty((batch, 12), dtype=torch.float32, device=device))
+        if full:
+            out.u = torch.empty((batch, 12 * N), dtype=torch.float32, device=device)
+        if stats:
+            out.status = torch.empty(batch, dtype=torch.int32, device=device)
+            out.iters = torch.empty(batch, dtype=torch.int32, device=device)
+            out.rho_updates = torch.empty(batch, dtype=torch.int32, device=device)
+            out.obj = torch.empty(batch, dtype=torch.float32, device=device)
+        return out
+
+    def solve(self, x0, x_ref, feet, contacts, out=None, full=False, max_legs=None,
+              warm=None, stream=None):
+        import torch
+        B = x0.shape[0]
+        N = self.spec.horizon
+        for name, t, dt in (("x0", x0, torch.float32), ("x_ref", x_ref, torch.float32),
+                            ("feet", feet, torch.float32), ("contacts", contacts, torch.uint8)):
+            if t.dtype != dt or not t.is_contiguous() or t.shape[0] != B:
+                raise ValueError("%s: need contiguous %s with batch %d" % (name, dt, B))
+            if not t.is_cuda:
+                raise ValueError("%s must be a device tensor (inputs resident in HBM)" % name)
+        if x0.shape[1] != 13 or x_ref.shape[1] != 13 * N:
+            raise ValueError("x0 (B,13) and x_ref (B,13N) expected")
+        self.spec.feet_per_step = 1 if feet.shape[1] == 12 * N and N > 1 else 0
+        self.spec.contacts_per_step = 1 if contacts.shape[1] == 4 * N and N > 1 else 0
+        if max_legs is None:
+            max_legs = max_stance_legs(contacts, N, bool(self.spec.contacts_per_step))
+        if out is None:
+            out = self.alloc_outputs(B, x0.device, full=full)
+        if stream is None:
+            stream = torch.cuda.current_stream(x0.device).cuda_stream
+        check(lib().qloco_srbd_solve_ex(
+            C.byref(self.spec), B, ptr(x0), ptr(x_ref), ptr(feet), ptr(contacts), ptr(out.u0),
+            ptr(out.u), ptr(out.status), ptr(out.iters), ptr(out.rho_updates), ptr(out.obj),
+            ptr(warm), int(max_legs), C.c_void_p(stream)), "qloco_srbd_solve")
+        return out

@@ -1,0 +1,237 @@
+"""ctypes binding of the CPU oracle (oracle/_build/libqloco_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "_build", "libqloco_oracle.so")
+
+_lib = None
+
+dp = C.POINTER(C.c_double)
+fp = C.POINTER(C.c_float)
+ip = C.POINTER(C.c_int)
+u8p = C.POINTER(C.c_uint8)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+class SrbdSpec(C.Structure):
+    _fields_ = [("N", C.c_int), ("dt", C.c_double), ("mass", C.c_double),
+                ("inertia", C.c_double * 9), ("q_w", C.c_double * 13),
+                ("r_w", C.c_double * 12), ("mu", C.c_double),
+                ("fz_min", C.c_double), ("fz_max", C.c_double)]
+
+
+class AdmmSettings(C.Structure):
+    _fields_ = [("rho", C.c_double), ("sigma", C.c_double), ("alpha", C.c_double),
+                ("eps_abs", C.c_double), ("eps_rel", C.c_double),
+                ("eps_prim_inf", C.c_double), ("eps_dual_inf", C.c_double),
+                ("max_iter", C.c_int), ("check_termination", C.c_int),
+                ("scaling", C.c_int), ("adaptive_rho", C.c_int),
+                ("adaptive_rho_interval", C.c_int),
+                ("adaptive_rho_tolerance", C.c_double), ("warm_start", C.c_int)]
+
+
+class AdmmInfo(C.Structure):
+    _fields_ = [("iters", C.c_int), ("rho_updates", C.c_int), ("status", C.c_int),
+                ("obj", C.c_double), ("pri_res", C.c_double), ("dua_res", C.c_double),
+                ("rho_final", C.c_double)]
+
+
+class ForceParams(C.Structure):
+    _fields_ = [(k, C.c_double) for k in ("mass", "alpha", "beta", "gamma", "fz_max", "mu")]
+
+
+class DynState(C.Structure):
+    _fields_ = [("F_leg_ref", C.c_double * 12), ("F_leg_guess", C.c_double * 12),
+                ("grf_opt", C.c_double * 12), ("qp_solution", C.c_int),
+                ("ws", C.c_void_p)]
+
+
+NH = 4
+
+
+class BodyState(C.Structure):
+    _fields_ = [("tx", C.c_double * 27), ("nsum_mpc", C.c_int), ("nstepx", C.c_int),
+                ("dt_mpc", C.c_double), ("j_ini", C.c_double), ("mass", C.c_double),
+                ("g", C.c_double), ("a", C.c_double * 4), ("b", C.c_double * 2),
+                ("pps", C.c_double * (NH * 2)), ("pvs", C.c_double * (NH * 2)),
+                ("ppu", C.c_double * (NH * NH)), ("pvu", C.c_double * (NH * NH)),
+                ("ppu_2", C.c_double * (NH * NH)), ("pvu_2", C.c_double * (NH * NH)),
+                ("thetax_max", C.c_double), ("thetax_min", C.c_double),
+                ("thetay_max", C.c_double), ("thetay_min", C.c_double),
+                ("torque_max", C.c_double), ("torque_min", C.c_double),
+                ("zmpx_max", C.c_double), ("zmpx_min", C.c_double),
+                ("zmpy_max", C.c_double), ("zmpy_min", C.c_double),
+                ("Rthetax", C.c_double), ("Rthetay", C.c_double),
+                ("alphathetax", C.c_double), ("alphathetay", C.c_double),
+                ("beltathetax", C.c_double), ("beltathetay", C.c_double),
+                ("gama_zmpx", C.c_double), ("gama_zmpy", C.c_double),
+                ("thetaxk", C.c_double * 2), ("thetayk", C.c_double * 2),
+                ("V_ini", C.c_double * (2 * NH)),
+                ("thetax", C.c_double * NH), ("thetay", C.c_double * NH),
+                ("torquex_real", C.c_double * NH), ("torquey_real", C.c_double * NH),
+                ("zmpx_real", C.c_double * NH), ("zmpy_real", C.c_double * NH),
+                ("bjx1", C.c_int), ("bjx2", C.c_int), ("t_yu", C.c_int),
+                ("qp_solution", C.c_int), ("ws", C.c_void_p)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.qo_eqp_create.restype = C.c_void_p
+        L.qo_eqp_create.argtypes = [C.c_int] * 3
+        L.qo_eqp_destroy.argtypes = [C.c_void_p]
+        L.qo_eqp_solve.restype = C.c_double
+        L.qo_eqp_solve.argtypes = [C.c_void_p, dp, dp, dp, dp, dp, dp, dp, ip, ip]
+        L.qo_splitmix64.restype = C.c_uint64
+        L.qo_splitmix64.argtypes = [C.c_uint64]
+        L.qo_gen_srbd.argtypes = [C.c_uint64, C.c_int, C.c_double, C.c_int, C.c_int64,
+                                  C.c_int64, fp, fp, fp, u8p]
+        L.qo_srbd_build_instance.argtypes = [C.POINTER(SrbdSpec), dp, dp, dp, C.c_int, u8p,
+                                             C.c_int, dp, dp, dp, dp]
+        L.qo_srbd_qp_mats.argtypes = [C.POINTER(SrbdSpec), dp, dp, dp, dp, u8p, C.c_int,
+                                      dp, dp, dp, dp, dp, dp]
+        L.qo_srbd_constraints.argtypes = [C.POINTER(SrbdSpec), dp]
+        L.qo_srbd_A_c.argtypes = [C.c_double, dp]
+        L.qo_srbd_B_c.argtypes = [C.c_double, dp, dp, dp, dp]
+        L.qo_srbd_discretize.argtypes = [dp, dp, C.c_double, dp, dp]
+        L.qo_admm_settings_default.argtypes = [C.POINTER(AdmmSettings)]
+        L.qo_admm_solve.restype = C.c_int
+        L.qo_admm_solve.argtypes = [C.POINTER(AdmmSettings), C.c_int, C.c_int, dp, dp, dp, dp,
+                                    dp, dp, dp, C.POINTER(AdmmInfo)]
+        L.qo_exact_solve.restype = C.c_int
+        L.qo_exact_solve.argtypes = [C.c_int, C.c_int, dp, dp, dp, dp, dp, dp, ip]
+        L.qo_srbd_batch.restype = C.c_int
+        L.qo_srbd_batch.argtypes = [C.POINTER(SrbdSpec), C.POINTER(AdmmSettings), C.c_int,
+                                    C.c_int64, fp, fp, fp, C.c_int, u8p, C.c_int, dp, ip, ip,
+                                    dp, C.c_int, dp]
+        L.qo_force_params_default.argtypes = [C.POINTER(ForceParams)]
+        L.qo_dyn_init.argtypes = [C.POINTER(DynState)]
+        L.qo_dyn_free.argtypes = [C.POINTER(DynState)]
+        L.qo_force_distribution.argtypes = [C.POINTER(DynState), dp, dp, dp, C.c_int,
+                                            C.c_double, dp, dp]
+        L.qo_force_opt.restype = C.c_int
+        L.qo_force_opt.argtypes = [C.POINTER(DynState), C.POINTER(ForceParams), dp, dp, dp,
+                                   dp, dp, dp, C.c_int, C.c_int, C.c_double, ip, ip]
+        L.qo_compute_joint_torques.argtypes = [C.POINTER(DynState), dp, C.c_int, dp, dp, dp,
+                                               dp, C.c_int, dp]
+        L.qo_body_init.argtypes = [C.POINTER(BodyState)]
+        L.qo_body_free.argtypes = [C.POINTER(BodyState)]
+        L.qo_body_indexfind.restype = C.c_int
+        L.qo_body_indexfind.argtypes = [C.POINTER(BodyState), C.c_double]
+        L.qo_body_theta_mpc.restype = C.c_int
+        L.qo_body_theta_mpc.argtypes = [C.POINTER(BodyState), C.c_int, dp, dp, dp, dp, dp,
+                                        dp, dp, dp, ip]
+        _lib = L
+    return _lib
+
+
+def P(a, t=C.c_double):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+GO1_INERTIA = 2.0 * np.array([[0.0168352186, 0.0004636141, 0.0002367952],
+                              [0.0004636141, 0.0656071082, 3.6671e-05],
+                              [0.0002367952, 3.6671e-05, 0.0742720659]])
+Q_W = [20.0, 10.0, 1.0, 0.0, 0.0, 420.0, 0.05, 0.05, 0.05, 30.0, 30.0, 10.0, 0.0]
+R_W = [1e-7] * 12
+
+
+def srbd_spec(N=10, dt=0.0025, mass=12.0, inertia=GO1_INERTIA, q_w=Q_W, r_w=R_W, mu=0.3,
+              fz_min=0.0, fz_max=180.0):
+    s = SrbdSpec()
+    s.N = N
+    s.dt = dt
+    s.mass = mass
+    for i, v in enumerate(np.asarray(inertia, dtype=np.float64).T.ravel()):
+        s.inertia[i] = v
+    for i, v in enumerate(q_w):
+        s.q_w[i] = v
+    for i, v in enumerate(r_w):
+        s.r_w[i] = v
+    s.mu, s.fz_min, s.fz_max = mu, fz_min, fz_max
+    return s
+
+
+def admm_settings(**kw):
+    s = AdmmSettings()
+    lib().qo_admm_settings_default(C.byref(s))
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+def gen_srbd(seed, N, count, gait=0, first=0, dt=0.0025):
+    x0 = np.zeros((count, 13), np.float32)
+    xr = np.zeros((count, 13 * N), np.float32)
+    ft = np.zeros((count, 12), np.float32)
+    ct = np.zeros((count, 4 * N), np.uint8)
+    lib().qo_gen_srbd(seed, N, float(np.float32(dt)), gait, first, count, P(x0, C.c_float), P(xr, C.c_float),
+                      P(ft, C.c_float), P(ct, C.c_uint8))
+    return x0, xr, ft, ct
+
+
+def build_instance(spec, x0, xr, feet, contacts, contacts_per_step=1, feet_per_step=0):
+    N = spec.N
+    n, m = 12 * N, 20 * N
+    H = np.zeros((n, n))
+    g = np.zeros(n)
+    lb = np.zeros(m)
+    ub = np.zeros(m)
+    x0d = np.ascontiguousarray(x0, np.float64)
+    xrd = np.ascontiguousarray(xr, np.float64)
+    ftd = np.ascontiguousarray(feet, np.float64)
+    ct = np.ascontiguousarray(contacts, np.uint8)
+    lib().qo_srbd_build_instance(C.byref(spec), P(x0d), P(xrd), P(ftd), feet_per_step,
+                                 P(ct, C.c_uint8), contacts_per_step, P(H), P(g), P(lb), P(ub))
+    return H.T.copy(), g, lb, ub  # H is symmetric; .T converts col-major view
+
+
+def constraints(spec):
+    N = spec.N
+    Cm = np.zeros((12 * N, 20 * N))  # col-major storage of a 20N x 12N matrix
+    lib().qo_srbd_constraints(C.byref(spec), P(Cm))
+    return Cm.T.copy()  # (20N, 12N) row-major numpy
+
+
+def admm_solve(H, g, A, l, u, settings=None, x=None, y=None):
+    n, m = H.shape[0], A.shape[0]
+    settings = settings or admm_settings()
+    Hc = np.asfortranarray(H).ravel(order="F").copy()
+    Ac = np.asfortranarray(A).ravel(order="F").copy()
+    x = np.zeros(n) if x is None else x.astype(np.float64).copy()
+    y = np.zeros(m) if y is None else y.astype(np.float64).copy()
+    info = AdmmInfo()
+    g = np.ascontiguousarray(g, np.float64)
+    l = np.ascontiguousarray(l, np.float64)
+    u = np.ascontiguousarray(u, np.float64)
+    st = lib().qo_admm_solve(C.byref(settings), n, m, P(Hc), P(g), P(Ac), P(l), P(u), P(x),
+                             P(y), C.byref(info))
+    return x, y, info
+
+
+def exact_solve(H, g, A, l, u):
+    n, m = H.shape[0], A.shape[0]
+    Hc = np.asfortranarray(H).ravel(order="F").copy()
+    Ac = np.asfortranarray(A).ravel(order="F").copy()
+    x = np.zeros(n)
+    it = C.c_int(0)
+    g = np.ascontiguousarray(g, np.float64)
+    l = np.ascontiguousarray(l, np.float64)
+    u = np.ascontiguousarray(u, np.float64)
+    st = lib().qo_exact_solve(n, m, P(Hc), P(g), P(Ac), P(l), P(u), P(x), C.byref(it))
+    return x, st, it.value
