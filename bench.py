@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""bench.py -- batched Go1 SRBD convex-MPC solves on MI355X.
+
+Metric (BASELINE.json): "MPC QP solves/sec (Go1 SRBD N=10, 12 forces) at
+1/2/4/8 GPUs; p99 solve µs".  Workload at N=1 GPU: configs[1] = Go1 trot
+convex MPC N=10 fp32, batch 4096 per GPU.  One "step" = one pass of the hot
+path over the batch: ONE fused kernel launch (condensed-QP build + OSQP
+ADMM to termination + force extraction), inputs already resident in HBM;
+for N>1 GPUs each rank solves its own 4096 instances (weak scaling, the
+instance range is regenerated locally from (seed, global id)) and the solved
+contact forces are all-gathered over RCCL/xGMI inside the timed step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+                    [--horizon 10] [--gait trot] [--no-cpu-baseline]
+
+Rank 0 prints ONE JSON line.  Launch for N>1 GPUs:
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector == FP32 MFMA peak
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
+SEED = 20261015
+
+
+def srbd_flops(n, iters, rho_updates, horizon, checks):
+    """Executed useful FP32 flops of one solve of the fused kernel.
+
+    n            stance variables (3 x stance (step, leg) pairs)
+    build        P rows in closed form (~12 flop/entry) + 10 Ruiz passes (2 flop/entry)
+    factorise    Gauss-Jordan inverse, 2 n^3, plus P rebuild/scale (14 n^2), per (1 + rho_updates)
+    iteration    K^-1 matvec 2 n^2 + ~30 n vector/row work
+    check        structured P x and norms, ~70 n, every check_termination (and rho) iteration
+    """
+    n = np.asarray(n, dtype=np.float64)
+    it = np.asarray(iters, dtype=np.float64)
+    ru = np.asarray(rho_updates, dtype=np.float64)
+    ch = np.asarray(checks, dtype=np.float64)
+    build = 12.0 * n * n + 20.0 * n * n + 40.0 * n + 60.0 * horizon
+    fac = (1.0 + ru) * (2.0 * n ** 3 + 14.0 * n * n)
+    iters = it * (2.0 * n * n + 30.0 * n)
+    chk = ch * 70.0 * n
+    return build + fac + iters + chk
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
+    ap.add_argument("--horizon", type=int, default=10)
+    ap.add_argument("--gait", default="trot")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-allgather", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from quadrupedal_loco_amd import srbd
+
+    B, N = args.batch, args.horizon
+    from quadrupedal_loco_amd.dist import shard_range
+    first, _ = shard_range(B, rank)
+    x0, xr, ft, ct = srbd.generate(SEED, N, B, args.gait, first=first)
+    d_x0 = torch.from_numpy(x0).to(dev)
+    d_xr = torch.from_numpy(xr).to(dev)
+    d_ft = torch.from_numpy(ft).to(dev)
+    d_ct = torch.from_numpy(ct).to(dev)
+    solver = srbd.BatchedConvexMpc(horizon=N)
+    legs = srbd.max_stance_legs(ct, N)
+    out = solver.alloc_outputs(B, dev)
+    gather = None
+    if world > 1 and not args.no_allgather:
+        from quadrupedal_loco_amd.dist import ForceGather
+        gather = ForceGather(B, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, max_legs=legs, stream=stream.cuda_stream)
+        if gather is not None:
+            gather(out.u0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    K = args.steps
+    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ev_k = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev_s[i].record(stream)
+        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, max_legs=legs, stream=stream.cuda_stream)
+        ev_k[i].record(stream)
+        if gather is not None:
+            gather(out.u0)
+        ev_e[i].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    kern_ms = np.array([ev_s[i].elapsed_time(ev_k[i]) for i in range(K)])
+    step_ms = np.array([ev_s[i].elapsed_time(ev_e[i]) for i in range(K)])
+
+    # per-instance stats of the solved batch (identical every step)
+    status = out.status.cpu().numpy()
+    iters = out.iters.cpu().numpy()
+    rho_up = out.rho_updates.cpu().numpy()
+    n_var = 3 * ct.reshape(B, -1).sum(axis=1)
+    checks = iters // 25 + iters // 100
+    flops = srbd_flops(n_var, iters, rho_up, N, checks)
+    flops_launch = float(flops.sum())
+    achieved_tflops = flops_launch / (kern_ms.mean() * 1e-3) / 1e12
+
+    value = B * world * K / elapsed
+    res = {
+        "metric": "MPC QP solves/sec (Go1 SRBD N=%d, 12 forces); p99 solve us" % N,
+        "value": round(value, 1),
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (counter-based generator, seed %d, DESIGN.md §4)" % SEED,
+        "config": {
+            "workload": "Go1 %s convex MPC N=%d fp32, batch=%d per GPU (BASELINE configs[1])"
+                        % (args.gait, N, B),
+            "horizon": N, "batch_per_gpu": B, "gait": args.gait,
+            "solver": "OSQP-algorithm ADMM, default settings (eps 1e-3, adaptive rho)",
+            "parallelism": "dp%d (instance shards, RCCL all-gather of u0)" % world,
+        },
+        "p99_batch_us": round(float(np.percentile(step_ms, 99)) * 1e3, 2),
+        "p50_batch_us": round(float(np.percentile(step_ms, 50)) * 1e3, 2),
+        "kernel_us_avg": round(float(kern_ms.mean()) * 1e3, 2),
+        "admm_iters_p50_p99": [int(np.percentile(iters, 50)), int(np.percentile(iters, 99))],
+        "status_ok_frac": float(np.mean(status == 0)),
+        "roofline": {
+            "bound": "mfma",
+            "achieved": round(achieved_tflops, 3),
+            "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4),
+            "traffic": None,
+            "note": "FP32 compute-bound (VALU; FP32 vector peak == FP32 MFMA peak 157.3 TF); "
+                    "flops = executed useful flops per launch (%.3g), DESIGN.md §5" % flops_launch,
+        },
+    }
+    tfile = os.path.join(ROOT, "profiles", "traffic_srbd_n%d_b%d.json" % (N, B))
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            res["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(N, args.gait, args.cpu_seconds, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(N, gait, seconds, threads):
+    """CPU-A baseline: the oracle's literal ConvexMpc build + OSQP-algorithm
+    ADMM restatement (double, full 12N-variable QP) on host threads, over a
+    bounded sample of the same synthetic workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+    import oracle_lib as O
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    sp = O.srbd_spec(N=N)
+    st = O.admm_settings()
+    g = {"trot": 0, "pace": 1, "mixed": 2, "stance": 3}.get(gait, 0)
+
+    def run(count):
+        x0, xr, ft, ct = O.gen_srbd(SEED, N, count, gait=g)
+        secs = C.c_double(0)
+        O.lib().qo_srbd_batch(C.byref(sp), C.byref(st), 0, count, O.P(x0, C.c_float),
+                              O.P(xr, C.c_float), O.P(ft, C.c_float), 0, O.P(ct, C.c_uint8), 1,
+                              None, None, None, None, threads, C.byref(secs))
+        return secs.value
+
+    probe = 4 * threads
+    tp = run(probe)
+    count = int(max(probe, min(2_000_000, probe * seconds / max(tp, 1e-6))))
+    t = run(count)
+    return {"value": round(count / t, 1), "unit": "solves/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d instances of the same workload (first %d of the seed), oracle CPU-A "
+                      "(literal dense ConvexMpc build + OSQP-algorithm ADMM, fp64), %.1f s"
+                      % (count, count, t)}
+
+
+if __name__ == "__main__":
+    main()

@@ -106,15 +106,51 @@ typedef struct {
   int *ctype;
   double *K;                   /* Cholesky factor of the reduced KKT */
   double rho, sigma;
+  /* A in CSC (OSQP stores A sparse): column j has rows ai[ap[j]..ap[j+1]) */
+  int *ap, *ai;
+  double *ax;
 } admm_ws;
 
+/* refresh the CSC values from the (scaled) dense A */
+static void csc_build(admm_ws *w) {
+  int nnz = 0;
+  for (int j = 0; j < w->n; ++j) {
+    w->ap[j] = nnz;
+    for (int i = 0; i < w->m; ++i) {
+      double a = w->A[(size_t)j * w->m + i];
+      if (a != 0.0) { w->ai[nnz] = i; w->ax[nnz] = a; nnz++; }
+    }
+  }
+  w->ap[w->n] = nnz;
+}
+static void csc_Ax(const admm_ws *w, const double *x, double *y) {
+  for (int i = 0; i < w->m; ++i) y[i] = 0.0;
+  for (int j = 0; j < w->n; ++j)
+    for (int k = w->ap[j]; k < w->ap[j + 1]; ++k) y[w->ai[k]] += w->ax[k] * x[j];
+}
+static void csc_Aty(const admm_ws *w, const double *y, double *x) {
+  for (int j = 0; j < w->n; ++j) {
+    double a = 0.0;
+    for (int k = w->ap[j]; k < w->ap[j + 1]; ++k) a += w->ax[k] * y[w->ai[k]];
+    x[j] = a;
+  }
+}
+
 static void build_factor(admm_ws *w) {
-  int n = w->n, m = w->m;
+  int n = w->n;
+  for (int c = 0; c < n; ++c)
+    for (int r = 0; r < n; ++r) w->K[(size_t)c * n + r] = w->P[(size_t)c * n + r] + (r == c ? w->sigma : 0.0);
+  /* + A' diag(rho) A: sum over rows shared by columns r, c */
   for (int c = 0; c < n; ++c)
     for (int r = 0; r < n; ++r) {
-      double a = w->P[(size_t)c * n + r] + (r == c ? w->sigma : 0.0);
-      for (int i = 0; i < m; ++i) a += w->A[(size_t)r * m + i] * w->rho_vec[i] * w->A[(size_t)c * m + i];
-      w->K[(size_t)c * n + r] = a;
+      int kr = w->ap[r], kc = w->ap[c];
+      double a = 0.0;
+      while (kr < w->ap[r + 1] && kc < w->ap[c + 1]) {
+        if (w->ai[kr] == w->ai[kc]) { a += w->ax[kr] * w->rho_vec[w->ai[kr]] * w->ax[kc]; kr++; kc++; }
+        else if (w->ai[kr] < w->ai[kc]) kr++;
+        else kc++;
+      }
+      w->K[(size_t)c * n + r] += a;
     }
   chol(n, w->K);
 }
@@ -217,6 +253,9 @@ int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P0, co
   w->rho_vec = (double *)malloc(sizeof(double) * m); w->rho_inv = (double *)malloc(sizeof(double) * m);
   w->ctype = (int *)malloc(sizeof(int) * m);
   w->K = (double *)malloc(sizeof(double) * (size_t)n * n);
+  w->ap = (int *)malloc(sizeof(int) * (n + 1));
+  w->ai = (int *)malloc(sizeof(int) * (size_t)m * n);
+  w->ax = (double *)malloc(sizeof(double) * (size_t)m * n);
   double *x = (double *)calloc(n, sizeof(double)), *xp = (double *)calloc(n, sizeof(double));
   double *z = (double *)calloc(m, sizeof(double)), *zp = (double *)calloc(m, sizeof(double));
   double *y = (double *)calloc(m, sizeof(double)), *dy = (double *)calloc(m, sizeof(double));
@@ -234,6 +273,7 @@ int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P0, co
     for (int j = 0; j < n; ++j) w->D[j] = w->Dinv[j] = 1.0;
     for (int i = 0; i < m; ++i) w->E[i] = w->Einv[i] = 1.0;
   }
+  csc_build(w);
   set_rho_vec(w);
   build_factor(w);
   int interval = st->adaptive_rho_interval;
@@ -243,11 +283,7 @@ int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P0, co
   if (st->warm_start) { /* osqp_warm_start: scale x by Dinv, y by Einv*c */
     for (int j = 0; j < n; ++j) x[j] = xo[j] * w->Dinv[j];
     for (int i = 0; i < m; ++i) y[i] = yo[i] * w->Einv[i] * w->c;
-    for (int i = 0; i < m; ++i) {
-      double a = 0.0;
-      for (int j = 0; j < n; ++j) a += w->A[(size_t)j * m + i] * x[j];
-      z[i] = a;
-    }
+    csc_Ax(w, x, z);
   }
 
   int iter, status = QO_MAX_ITER, can_check = 0, rho_updates = 0;
@@ -255,20 +291,15 @@ int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P0, co
   /* residuals in the scaled space + their unscaled norms (update_info) */
 #define UPDATE_INFO()                                                                    \
   do {                                                                                   \
-    for (int i = 0; i < m; ++i) {                                                        \
-      double a = 0.0;                                                                    \
-      for (int j = 0; j < n; ++j) a += w->A[(size_t)j * m + i] * x[j];                   \
-      Ax[i] = a;                                                                         \
-      rp[i] = a - z[i];                                                                  \
-    }                                                                                    \
+    csc_Ax(w, x, Ax);                                                                    \
+    for (int i = 0; i < m; ++i) rp[i] = Ax[i] - z[i];                                    \
     pri_res = vsnorm(w->Einv, rp, m);                                                    \
+    csc_Aty(w, y, Aty);                                                                  \
     for (int j = 0; j < n; ++j) {                                                        \
-      double a = 0.0, b = 0.0;                                                           \
+      double a = 0.0;                                                                    \
       for (int r = 0; r < n; ++r) a += w->P[(size_t)r * n + j] * x[r];                   \
-      for (int i = 0; i < m; ++i) b += w->A[(size_t)j * m + i] * y[i];                   \
       Px[j] = a;                                                                         \
-      Aty[j] = b;                                                                        \
-      rd[j] = w->q[j] + a + b;                                                           \
+      rd[j] = w->q[j] + a + Aty[j];                                                      \
     }                                                                                    \
     dua_res = w->cinv * vsnorm(w->Dinv, rd, n);                                          \
   } while (0)
@@ -277,17 +308,11 @@ int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P0, co
     memcpy(xp, x, sizeof(double) * n);
     memcpy(zp, z, sizeof(double) * m);
     /* update_xz_tilde (reduced KKT) */
-    for (int j = 0; j < n; ++j) {
-      double a = w->sigma * xp[j] - w->q[j];
-      for (int i = 0; i < m; ++i) a += w->A[(size_t)j * m + i] * (w->rho_vec[i] * zp[i] - y[i]);
-      xt[j] = a;
-    }
+    for (int i = 0; i < m; ++i) tm[i] = w->rho_vec[i] * zp[i] - y[i];
+    csc_Aty(w, tm, xt);
+    for (int j = 0; j < n; ++j) xt[j] += w->sigma * xp[j] - w->q[j];
     chol_solve(n, w->K, xt);
-    for (int i = 0; i < m; ++i) {
-      double a = 0.0;
-      for (int j = 0; j < n; ++j) a += w->A[(size_t)j * m + i] * xt[j];
-      zt[i] = a;
-    }
+    csc_Ax(w, xt, zt);
     /* update_x, update_z, update_y */
     for (int j = 0; j < n; ++j) {
       x[j] = st->alpha * xt[j] + (1.0 - st->alpha) * xp[j];
@@ -355,6 +380,7 @@ int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P0, co
   }
   free(w->P); free(w->q); free(w->A); free(w->l); free(w->u); free(w->D); free(w->Dinv);
   free(w->E); free(w->Einv); free(w->rho_vec); free(w->rho_inv); free(w->ctype); free(w->K);
+  free(w->ap); free(w->ai); free(w->ax);
   free(x); free(xp); free(z); free(zp); free(y); free(dy); free(dx); free(xt); free(zt);
   free(Ax); free(Px); free(Aty); free(rp); free(rd); free(tm);
   return status;

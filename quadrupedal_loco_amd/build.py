@@ -21,8 +21,15 @@ ARCH = "gfx950"
 SOURCES = [
     "qloco_capi.hip",
     "qloco_srbd.hip",
+    "qloco_gi.hip",
+    "qloco_force.hip",
+    "qloco_body.hip",
     "qloco_gen.cpp",
 ]
+# per-file extra flags: the fp64 active-set kernel keeps the restatement's
+# exact operation sequence (no FMA contraction)
+EXTRA = {"qloco_gi.hip": ["-ffp-contract=off"], "qloco_force.hip": ["-ffp-contract=off"],
+         "qloco_body.hip": ["-ffp-contract=off"]}
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC]
 
@@ -46,7 +53,8 @@ def build(verbose=False, jobs=8):
         if not _needs(obj, [path] + headers):
             continue
         if src.endswith(".hip"):
-            cmd = [HIPCC, "--offload-arch=" + ARCH, "-x", "hip"] + COMMON + ["-c", path, "-o", obj]
+            cmd = ([HIPCC, "--offload-arch=" + ARCH, "-x", "hip"] + COMMON + EXTRA.get(src, []) +
+                   ["-c", path, "-o", obj])
         else:  # host-only C++ (generator): exact IEEE, no contraction
             cmd = [HIPCC, "-x", "c++"] + COMMON + ["-ffp-contract=off", "-c", path, "-o", obj]
         cmds.append(cmd)

@@ -1,0 +1,401 @@
+// qloco_body.hip -- batched rt body-inclination MPC step (gfx950).
+//
+// Replaces PRMPCClass::body_theta_mpc (rt_mpc_qp/src/FastMPC/
+// PRMPCClass.cpp:379-714) + Indexfind (:716-738) + solve_body_rotation /
+// Solve (:799-849), called at 100 Hz from gait_fast.cpp:620.  Constants of
+// PRMPCClass::Initialize (:157-374) are computed once on the host
+// (body_constants) and passed by value.  One instance per 16-lane group:
+// the group derives the schedule integers (bjx1, bjx2, t_yu -- fp64 compares,
+// bit-exact), builds the 8-variable QP in LDS, solves it with the
+// Goldfarb-Idnani core and applies the reference's clamping, propagation and
+// (all-zero) lambda feedback.  The 16 CI columns the reference never writes
+// (:813-816, :826-829) are zero, i.e. inert.
+#include <math.h>
+#include <string.h>
+
+#include "qloco_gi_core.hpp"
+
+namespace qloco {
+
+constexpr int BNH = 4;               // _nh
+constexpr int BNT = 2 * BNH;         // _Nt
+constexpr int BNI = 12 * BNH;        // resizeQP(_Nt, 0, 12*_nh)
+constexpr int BSTEPS = 27;           // _footstepsnumber
+
+struct BodyConsts {
+  double tx[BSTEPS];
+  int nsum_mpc, nstepx;
+  double dt_mpc, j_ini, mass, g;
+  double a[4], b[2];
+  double pps[BNH * 2], pvs[BNH * 2], ppu[BNH * BNH], pvu[BNH * BNH], ppu_2[BNH * BNH],
+      pvu_2[BNH * BNH];
+  double thetax_max, thetax_min, thetay_max, thetay_min, torque_max, torque_min;
+  double Rthetax, Rthetay, alphathetax, alphathetay, beltathetax, beltathetay, gama_zmpx,
+      gama_zmpy;
+};
+
+static void mat2_mul(const double A[4], const double B[4], double C[4]) {
+  const double c00 = A[0] * B[0] + A[2] * B[1];
+  const double c10 = A[1] * B[0] + A[3] * B[1];
+  const double c01 = A[0] * B[2] + A[2] * B[3];
+  const double c11 = A[1] * B[2] + A[3] * B[3];
+  C[0] = c00;
+  C[1] = c10;
+  C[2] = c01;
+  C[3] = c11;
+}
+
+// PRMPCClass::Initialize, QP part (PRMPCClass.cpp:157-374) with the gait::
+// constants of rt_mpc_qp/src/Robotpara/robot_const_para_config.cpp:8-47.
+static void body_constants(BodyConsts &c) {
+  memset(&c, 0, sizeof(c));
+  const double dt_slow = 0.025, dt_fast = 0.01, tstep = 0.7;
+  c.dt_mpc = dt_fast;
+  c.j_ini = 12 * 0.1 * 0.1;
+  c.mass = 12;
+  c.g = 9.8;
+  c.tx[0] = 0.0;
+  for (int i = 1; i < BSTEPS; i++) {  // :174-178
+    c.tx[i] = c.tx[i - 1] + tstep;
+    c.tx[i] = round(c.tx[i] / dt_slow) * dt_slow - 0.00001;
+  }
+  c.nstepx = (int)round(tstep / dt_fast);                   // :172
+  c.nsum_mpc = (int)floor(c.tx[BSTEPS - 1] / dt_fast);      // :185
+  c.a[0] = 1;
+  c.a[1] = 0;
+  c.a[2] = dt_fast;
+  c.a[3] = 1;
+  c.b[0] = pow(dt_fast, 2) / 2;
+  c.b[1] = dt_fast;
+  const double cp[2] = {1, 0}, cv[2] = {0, 1};
+  for (int pass = 0; pass < 2; ++pass) {  // Matrix_ps (:741-763)
+    const double *cc = pass == 0 ? cp : cv;
+    double *out = pass == 0 ? c.pps : c.pvs;
+    for (int i = 0; i < BNH; i++) {
+      double A[4] = {1, 0, 0, 1};
+      for (int j = 1; j < i + 2; j++) mat2_mul(A, c.a, A);
+      out[0 * BNH + i] = cc[0] * A[0] + cc[1] * A[1];
+      out[1 * BNH + i] = cc[0] * A[2] + cc[1] * A[3];
+    }
+  }
+  for (int pass = 0; pass < 2; ++pass) {  // Matrix_pu (:765-796)
+    const double *cc = pass == 0 ? cp : cv;
+    double *out = pass == 0 ? c.ppu : c.pvu;
+    for (int i = 1; i < BNH + 1; i++)
+      for (int j = 1; j < i + 1; j++) {
+        double A[4] = {1, 0, 0, 1};
+        if (j != i)
+          for (int k = 1; k < i - j + 1; k++) mat2_mul(A, c.a, A);
+        const double ca0 = cc[0] * A[0] + cc[1] * A[1];
+        const double ca1 = cc[0] * A[2] + cc[1] * A[3];
+        out[(j - 1) * BNH + (i - 1)] = ca0 * c.b[0] + ca1 * c.b[1];
+      }
+  }
+  for (int cc = 0; cc < BNH; ++cc)  // :219-220
+    for (int r = 0; r < BNH; ++r) {
+      double a1 = 0, a2 = 0;
+      for (int k = 0; k < BNH; ++k) {
+        a1 += c.pvu[r * BNH + k] * c.pvu[cc * BNH + k];
+        a2 += c.ppu[r * BNH + k] * c.ppu[cc * BNH + k];
+      }
+      c.pvu_2[cc * BNH + r] = a1;
+      c.ppu_2[cc * BNH + r] = a2;
+    }
+  c.thetax_max = 10 * M_PI / 180;
+  c.thetax_min = -10 * M_PI / 180;
+  c.thetay_max = 10 * M_PI / 180;
+  c.thetay_min = -10 * M_PI / 180;
+  c.torque_max = 20 / c.j_ini;
+  c.torque_min = -20 / c.j_ini;
+  c.Rthetax = 100;  // go1 weights, :280-287
+  c.Rthetay = 100;
+  c.alphathetax = 10;
+  c.alphathetay = 10;
+  c.beltathetax = 5000000000.0;
+  c.beltathetay = 5000000000.0;
+  c.gama_zmpx = 5000;
+  c.gama_zmpy = 5000;
+}
+
+struct BodyArgs {
+  BodyConsts k;
+  int64_t batch;
+  const int *i;
+  const double *bodyangle_state, *zmp_ref, *angle_ref, *rfoot_ref, *lfoot_ref, *comacc_ref;
+  double *state, *com_traj;
+  int *status;
+};
+
+struct BodyLds {
+  double CI[BNT * BNI];
+  struct Grp {
+    double G[BNT * BNT], g0[BNT], ci0[BNI], x[16];
+    GiLds gi;
+  } g[GI_GROUPS];
+};
+
+// PRMPCClass::Indexfind, xyz = 0 branch (:716-738)
+__device__ __forceinline__ int indexfind(const BodyConsts &k, double goal) {
+  int j = 0;
+  while (j < BSTEPS && goal >= k.tx[j]) j++;
+  return j - 1;
+}
+
+#define R2(m, r, c) ((m)[(c)*2 + (r)])
+#define R3(m, r, c) ((m)[(c)*3 + (r)])
+
+__global__ __launch_bounds__(64) void body_mpc_kernel(const BodyArgs a) {
+  __shared__ BodyLds S;
+  const BodyConsts &K = a.k;
+  const int lane = threadIdx.x, grp = lane >> 4, li = lane & 15;
+  const int64_t inst = (int64_t)blockIdx.x * GI_GROUPS + grp;
+  // constant rows (:541-561, :805-812): CI(:, c) = -[q_upx' q_lowx' q_upy'
+  // q_lowy' t_upx' t_lowx' t_upy' t_lowy'], columns 32..47 zero
+  for (int t = lane; t < BNT * BNI; t += 64) S.CI[t] = 0.0;
+  __syncthreads();
+  if (lane < BNH) {
+    const int row = lane;
+    for (int v = 0; v < BNH; ++v) {
+      const double pu = K.ppu[v * BNH + row];
+      S.CI[(0 * BNH + row) * BNT + v] = -pu;
+      S.CI[(1 * BNH + row) * BNT + v] = pu;
+      S.CI[(2 * BNH + row) * BNT + BNH + v] = -pu;
+      S.CI[(3 * BNH + row) * BNT + BNH + v] = pu;
+    }
+    S.CI[(4 * BNH + row) * BNT + row] = -K.j_ini;
+    S.CI[(5 * BNH + row) * BNT + row] = K.j_ini;
+    S.CI[(6 * BNH + row) * BNT + BNH + row] = -K.j_ini;
+    S.CI[(7 * BNH + row) * BNT + BNH + row] = K.j_ini;
+  }
+  __syncthreads();
+  if (inst >= a.batch) return;
+  BodyLds::Grp &P = S.g[grp];
+  double *st = a.state + inst * QLOCO_BODY_STATE_LEN;
+  const double *zmp_ref = a.zmp_ref + inst * 10, *angle_ref = a.angle_ref + inst * 10;
+  const double *rfoot_ref = a.rfoot_ref + inst * 10, *lfoot_ref = a.lfoot_ref + inst * 10;
+  const double *comacc_ref = a.comacc_ref + inst * 15;
+  double thetaxk[2] = {st[0], st[1]}, thetayk[2] = {st[2], st[3]};
+  int i = a.i[inst];
+  int status = QLOCO_OK;
+  bool active = false;
+  const int off = (int)round(1.0 / K.dt_mpc);  // height_offset_time / dt (:395)
+  int bjx1 = (int)st[26], bjx2 = (int)st[27], t_yu = (int)st[28];
+  if (i >= off) {
+    i -= off;
+    active = i < (K.nsum_mpc - BNH);  // :403
+  }
+  if (active) {
+    const double t_f0 = (i + 1) * K.dt_mpc, t_f3 = (i + BNH) * K.dt_mpc;  // :406
+    bjx1 = indexfind(K, t_f0) + 1;
+    bjx2 = indexfind(K, t_f3) + 1;
+    t_yu = (i + 1) % K.nstepx;
+    double copx[BNH], copy[BNH];
+    const double *sup = lfoot_ref, *oth = rfoot_ref;  // CoP reference, :427-499
+    if (bjx1 >= 2 && (bjx1 % 2 != 0)) {
+      sup = rfoot_ref;
+      oth = lfoot_ref;
+    }
+    for (int k = 0; k < BNH; ++k) {
+      copx[k] = R2(sup, 0, k);
+      copy[k] = R2(sup, 1, k);
+    }
+    if (bjx1 >= 2 && !((t_yu + BNH - 1) < K.nstepx)) {
+      const int t_yu_k = (t_yu + BNH) - K.nstepx;
+      for (int jx = 1; jx <= t_yu_k; jx++) {
+        copx[BNH - jx] = R2(oth, 0, BNH - jx);
+        copy[BNH - jx] = R2(oth, 1, BNH - jx);
+      }
+    }
+    double pth[BNH];
+    for (int jx = 0; jx < BNH; jx++) pth[jx] = K.j_ini / (K.mass * (R3(comacc_ref, 2, jx) + K.g));
+    if (li == 0) {
+      for (int t = 0; t < BNT * BNT; ++t) P.G[t] = 0.0;
+      for (int c = 0; c < BNH; ++c)
+        for (int r = 0; r < BNH; ++r) {  // :511-515
+          const double I = (r == c) ? 1.0 : 0.0;
+          double pp = pth[r] * pth[c];
+          if (r != c) pp = 0.0;
+          const double wx = K.Rthetax / 2 * I + K.alphathetax / 2 * K.pvu_2[c * BNH + r] +
+                            K.beltathetax / 2 * K.ppu_2[c * BNH + r] + K.gama_zmpy / 2 * pp;
+          const double wy = K.Rthetay / 2 * I + K.alphathetay / 2 * K.pvu_2[c * BNH + r] +
+                            K.beltathetay / 2 * K.ppu_2[c * BNH + r] + K.gama_zmpx / 2 * pp;
+          P.G[c * BNT + r] = 2 * wx;
+          P.G[(c + BNH) * BNT + (r + BNH)] = 2 * wy;
+        }
+      double det_px[BNH], det_py[BNH];
+      for (int k = 0; k < BNH; ++k) {
+        det_px[k] = R2(zmp_ref, 0, k) - copx[k];
+        det_py[k] = R2(zmp_ref, 1, k) - copy[k];
+      }
+      for (int r = 0; r < BNH; ++r) {  // q_goal, :523-526
+        double pvs_tx, pps_tx, pvs_ty, pps_ty;
+        double vx = 0, px = 0, vy = 0, py = 0, refx = 0, refy = 0;
+        for (int k = 0; k < BNH; ++k) {
+          pvs_tx = K.pvs[k] * thetaxk[0] + K.pvs[BNH + k] * thetaxk[1];
+          pps_tx = K.pps[k] * thetaxk[0] + K.pps[BNH + k] * thetaxk[1];
+          pvs_ty = K.pvs[k] * thetayk[0] + K.pvs[BNH + k] * thetayk[1];
+          pps_ty = K.pps[k] * thetayk[0] + K.pps[BNH + k] * thetayk[1];
+          vx += K.pvu[r * BNH + k] * pvs_tx;
+          px += K.ppu[r * BNH + k] * pps_tx;
+          vy += K.pvu[r * BNH + k] * pvs_ty;
+          py += K.ppu[r * BNH + k] * pps_ty;
+          refx += K.ppu[r * BNH + k] * R2(angle_ref, 0, k);
+          refy += K.ppu[r * BNH + k] * R2(angle_ref, 1, k);
+        }
+        P.g0[r] = K.alphathetax * vx + K.beltathetax * px - K.beltathetax * refx +
+                  K.gama_zmpy * pth[r] * det_py[r];
+        P.g0[BNH + r] = K.alphathetay * vy + K.beltathetay * py - K.beltathetay * refy +
+                        K.gama_zmpx * (-pth[r]) * det_px[r];
+      }
+      for (int t = 0; t < BNI; ++t) P.ci0[t] = 0.0;
+      for (int row = 0; row < BNH; ++row) {
+        const double ppsx = K.pps[row] * thetaxk[0] + K.pps[BNH + row] * thetaxk[1];
+        const double ppsy = K.pps[row] * thetayk[0] + K.pps[BNH + row] * thetayk[1];
+        P.ci0[0 * BNH + row] = K.thetax_max - ppsx;
+        P.ci0[1 * BNH + row] = -K.thetax_min + ppsx;
+        P.ci0[2 * BNH + row] = K.thetay_max - ppsy;
+        P.ci0[3 * BNH + row] = -K.thetay_min + ppsy;
+        P.ci0[4 * BNH + row] = K.torque_max;
+        P.ci0[5 * BNH + row] = -K.torque_min;
+        P.ci0[6 * BNH + row] = K.torque_max;
+        P.ci0[7 * BNH + row] = -K.torque_min;
+      }
+    }
+    GI_SYNC();
+    double f;
+    int it;
+    gi_solve_group(P.gi, li, BNT, 0, BNI, P.G, BNT, P.g0, nullptr, nullptr, S.CI, P.ci0, P.x, f,
+                   status, it);
+    GI_SYNC();
+    if (li == 0) {
+      bool ok = true;
+      for (int k = 0; k < BNT; ++k) ok = ok && !isnan(P.x[k]);
+      double V[BNT];
+      for (int k = 0; k < BNT; ++k) V[k] = P.x[k];  // Solve: _V_ini = _X (:844-847)
+      const double *aa = K.a, *bb = K.b;
+      double thax0 = V[0], thay0 = V[BNH];
+      const double a0x = aa[0] * thetaxk[0] + aa[2] * thetaxk[1];
+      const double a0y = aa[0] * thetayk[0] + aa[2] * thetayk[1];
+      if (!ok) {  // :570-579
+        thax0 = (thetaxk[0] - a0x) / bb[0];
+        thay0 = (thetayk[0] - a0y) / bb[0];
+      } else {  // :580-617
+        const double nx0 = a0x + bb[0] * thax0;
+        if (nx0 > K.thetax_max) thax0 = (K.thetax_max - a0x) / bb[0];
+        else if (nx0 < K.thetax_min) thax0 = (K.thetax_min - a0x) / bb[0];
+        const double ny0 = a0y + bb[0] * thay0;
+        if (ny0 > K.thetay_max) thay0 = (K.thetay_max - a0y) / bb[0];
+        else if (ny0 < K.thetay_min) thay0 = (K.thetay_min - a0y) / bb[0];
+      }
+      V[0] = thax0;
+      V[BNH] = thay0;
+      const double txk_tmp[2] = {aa[0] * thetaxk[0] + aa[2] * thetaxk[1] + bb[0] * thax0,
+                                 aa[1] * thetaxk[0] + aa[3] * thetaxk[1] + bb[1] * thax0};
+      const double tyk_tmp[2] = {aa[0] * thetayk[0] + aa[2] * thetayk[1] + bb[0] * thay0,
+                                 aa[1] * thetayk[0] + aa[3] * thetayk[1] + bb[1] * thay0};
+      double thetax[BNH], thetay[BNH], zmpx[BNH], zmpy[BNH];
+      const double torquex0 = K.j_ini * thax0, torquey0 = K.j_ini * thay0;
+      for (int jj = 0; jj < BNH; jj++) {  // :636-655
+        const double tax = V[jj], tay = V[BNH + jj];
+        const double x0 = aa[0] * thetaxk[0] + aa[2] * thetaxk[1] + bb[0] * tax;
+        const double x1 = aa[1] * thetaxk[0] + aa[3] * thetaxk[1] + bb[1] * tax;
+        thetaxk[0] = x0;
+        thetaxk[1] = x1;
+        thetax[jj] = x0;
+        const double y0 = aa[0] * thetayk[0] + aa[2] * thetayk[1] + bb[0] * tay;
+        const double y1 = aa[1] * thetayk[0] + aa[3] * thetayk[1] + bb[1] * tay;
+        thetayk[0] = y0;
+        thetayk[1] = y1;
+        thetay[jj] = y0;
+        const double den = K.mass * (K.g + R3(comacc_ref, 2, jj));
+        zmpx[jj] = R2(zmp_ref, 0, jj) - K.j_ini * tay / den;
+        zmpy[jj] = R2(zmp_ref, 1, jj) + K.j_ini * tax / den;
+      }
+      thetaxk[0] = txk_tmp[0];
+      thetaxk[1] = txk_tmp[1];
+      thetayk[0] = tyk_tmp[0];
+      thetayk[1] = tyk_tmp[1];
+      const double *bs = a.bodyangle_state + inst * 4;  // lambda feedback, all 0 (:664-692)
+      const double lx = 0.0, lvx = 0.0, ly = 0.0, lvy = 0.0;
+      thetaxk[0] = lx * bs[0] + (1 - lx) * thetaxk[0];
+      thetaxk[1] = lvx * bs[1] + (1 - lvx) * thetaxk[1];
+      thetayk[0] = (ly * bs[2] + (1 - ly) * thetayk[0]);
+      thetayk[1] = (lvy * bs[3] + (1 - lvy) * thetayk[1]);
+      st[0] = thetaxk[0];
+      st[1] = thetaxk[1];
+      st[2] = thetayk[0];
+      st[3] = thetayk[1];
+      for (int k = 0; k < BNT; ++k) st[4 + k] = V[k];
+      const double ct[14] = {thetax[0], thetay[0], torquex0, torquey0, zmpx[0], zmpy[0],
+                             thetax[1], thetay[1], zmpx[1],  zmpy[1],  thetax[2], thetay[2],
+                             zmpx[2],   zmpy[2]};
+      for (int k = 0; k < 14; ++k) st[12 + k] = ct[k];
+      st[26] = bjx1;
+      st[27] = bjx2;
+      st[28] = t_yu;
+      st[29] = ok ? 1.0 : 0.0;
+    }
+  }
+  GI_SYNC();
+  if (li < 14) a.com_traj[inst * 14 + li] = st[12 + li];  // :696-709 (last state otherwise)
+  if (li == 0 && a.status) a.status[inst] = active ? status : QLOCO_OK;
+}
+
+__global__ void indexfind_kernel(const BodyConsts k, int64_t batch, const double *t, int *j) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < batch) j[idx] = indexfind(k, t[idx]);
+}
+
+}  // namespace qloco
+
+using namespace qloco;
+
+extern "C" int qloco_body_state_init_host(int64_t batch, double *state) {
+  if (batch < 0 || (batch > 0 && !state)) return QLOCO_ERR_ARG;
+  memset(state, 0, sizeof(double) * QLOCO_BODY_STATE_LEN * batch);
+  for (int64_t b = 0; b < batch; ++b) state[b * QLOCO_BODY_STATE_LEN + 29] = 1.0;  // qp_solution
+  return QLOCO_OK;
+}
+
+extern "C" int qloco_body_mpc_step(int64_t batch, const int32_t *i,
+                                   const double *bodyangle_state, const double *zmp_ref,
+                                   const double *angle_ref, const double *rfoot_ref,
+                                   const double *lfoot_ref, const double *comacc_ref,
+                                   double *state, double *com_traj, int32_t *status,
+                                   void *stream) {
+  if (batch < 0) return QLOCO_ERR_ARG;
+  if (batch == 0) return QLOCO_OK;
+  if (!i || !bodyangle_state || !zmp_ref || !angle_ref || !rfoot_ref || !lfoot_ref ||
+      !comacc_ref || !state || !com_traj)
+    return QLOCO_ERR_ARG;
+  BodyArgs a;
+  memset(&a, 0, sizeof(a));
+  body_constants(a.k);
+  a.batch = batch;
+  a.i = i;
+  a.bodyangle_state = bodyangle_state;
+  a.zmp_ref = zmp_ref;
+  a.angle_ref = angle_ref;
+  a.rfoot_ref = rfoot_ref;
+  a.lfoot_ref = lfoot_ref;
+  a.comacc_ref = comacc_ref;
+  a.state = state;
+  a.com_traj = com_traj;
+  a.status = status;
+  const unsigned blocks = (unsigned)((batch + GI_GROUPS - 1) / GI_GROUPS);
+  hipLaunchKernelGGL(body_mpc_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+  QLOCO_HIP_CHECK(hipGetLastError(), "body_mpc_kernel launch");
+  return QLOCO_OK;
+}
+
+extern "C" int qloco_body_indexfind(int64_t batch, const double *t, int32_t *j_period,
+                                    void *stream) {
+  if (batch < 0 || (batch > 0 && (!t || !j_period))) return QLOCO_ERR_ARG;
+  if (batch == 0) return QLOCO_OK;
+  BodyConsts k;
+  body_constants(k);
+  hipLaunchKernelGGL(indexfind_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, k, batch, t, j_period);
+  QLOCO_HIP_CHECK(hipGetLastError(), "indexfind_kernel launch");
+  return QLOCO_OK;
+}

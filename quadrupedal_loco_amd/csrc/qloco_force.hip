@@ -1,0 +1,328 @@
+// qloco_force.hip -- batched Go1 force-distribution QP (gfx950).
+//
+// Replaces Dynamiccclass::force_distribution + force_opt + solve_grf_opt +
+// Solve (go1_rt_control/src/whole_body_dynamics/dynmics_compute.cpp:141-445),
+// called every 1 kHz servo tick at servo.cpp:1224-1228 (sim) and
+// torque_mode.cpp:1364-1367 (hardware).  One instance per 16-lane group:
+// the group builds G = 2(alpha A'A + (beta+gamma) I), g0, the swing-leg
+// equality pattern CE and the shared friction/bound rows CI in LDS, then
+// runs the Goldfarb-Idnani solver of qloco_gi_core.hpp on them.  The
+// skew_hat comma-operator bug (:379-381) and the F_prev = grf_opt coupling
+// (:305) are reproduced; a NaN solution falls back to F_leg_guess (:364-367).
+#include <string.h>
+
+#include "qloco_gi_core.hpp"
+
+namespace qloco {
+
+struct ForceArgs {
+  double mass, alpha, beta, gamma, fz_max, mu;
+  int64_t batch;
+  const double *com_des, *leg_des, *F_force_des, *rfoot_des, *lfoot_des;
+  const double *base_p, *feet_p, *FT_total_des, *y_coef;
+  const int *mode, *right_support;
+  double *F_leg_ref, *grf_opt, *F_leg_guess;
+  int *qp_solution, *status, *iters;
+};
+
+struct ForceLds {
+  double CI[12 * 24];  // shared by the four groups (constant rows)
+  double ci0[24];
+  double zeros[16];
+  struct Grp {
+    double G[144], g0[12], CE[144], A[72], x[16], guess[12];
+    GiLds gi;
+  } g[GI_GROUPS];
+};
+
+__device__ __forceinline__ double sq(double v) { return v * v; }
+
+// dynmics_compute.cpp:141-261 (scalar, executed redundantly by the group)
+__device__ void force_distribution(const double *com_des, const double *leg_des,
+                                   const double *F, int mode, double y_coefficient,
+                                   const double *rfoot_des, const double *lfoot_des,
+                                   double *R /* F_leg_ref 3x4 col-major, in/out */) {
+#define FRC(r, c) R[(c)*3 + (r)]
+  const double body_FR_dis = sqrt(sq(com_des[0] - leg_des[0]) + sq(com_des[1] - leg_des[1]) + sq(com_des[2] - leg_des[2]));
+  const double body_FL_dis = sqrt(sq(com_des[0] - leg_des[3]) + sq(com_des[1] - leg_des[4]) + sq(com_des[2] - leg_des[5]));
+  const double body_RR_dis = sqrt(sq(com_des[0] - leg_des[6]) + sq(com_des[1] - leg_des[7]) + sq(com_des[2] - leg_des[8]));
+  const double body_RL_dis = sqrt(sq(com_des[0] - leg_des[9]) + sq(com_des[1] - leg_des[10]) + sq(com_des[2] - leg_des[11]));
+  double f_double;
+  if (mode == 101) {
+    f_double = F[0] * body_FL_dis / (body_FL_dis + body_RL_dis);
+    FRC(0, 3) = f_double;
+    FRC(0, 1) = F[0] - f_double;
+    f_double = F[1] * body_FL_dis / (body_FL_dis + body_RL_dis) * y_coefficient;
+    FRC(1, 3) = f_double;
+    FRC(1, 1) = F[1] * y_coefficient - f_double;
+    f_double = F[2] * body_FL_dis / (body_FL_dis + body_RL_dis);
+    FRC(2, 3) = f_double;
+    FRC(2, 1) = F[2] - f_double;
+    f_double = F[3] * body_FR_dis / (body_FR_dis + body_RR_dis);
+    FRC(0, 2) = f_double;
+    FRC(0, 0) = F[3] - f_double;
+    f_double = F[4] * body_FR_dis / (body_FR_dis + body_RR_dis) * y_coefficient;
+    FRC(1, 2) = f_double;
+    FRC(1, 0) = F[4] * y_coefficient - f_double;
+    f_double = F[5] * body_FR_dis / (body_FR_dis + body_RR_dis);
+    FRC(2, 2) = f_double;
+    FRC(2, 0) = F[5] - f_double;
+  } else if (mode == 102) {
+    const double v0 = leg_des[9] - leg_des[0], v1 = leg_des[10] - leg_des[1], v2 = leg_des[11] - leg_des[2];
+    const double c0 = lfoot_des[0] - leg_des[0], c1 = lfoot_des[1] - leg_des[1], c2 = lfoot_des[2] - leg_des[2];
+    const double rlleg_dis = sqrt(sq(v0) + sq(v1) + sq(v2));
+    const double com_rleg_dis = v0 * c0 + v1 * c1 + v2 * c2;
+    const double raw = com_rleg_dis / rlleg_dis;
+    const double raw1 = raw < 1.0 ? raw : 1.0;
+    const double rleg_com = raw1 > 0.0 ? raw1 : 0.0;
+    f_double = F[0] * rleg_com;
+    FRC(0, 3) = f_double;
+    FRC(0, 0) = F[0] - f_double;
+    f_double = F[1] * rleg_com * y_coefficient;
+    FRC(1, 3) = f_double;
+    FRC(1, 0) = F[1] * y_coefficient - f_double;
+    f_double = F[2] * rleg_com;
+    FRC(2, 3) = f_double;
+    FRC(2, 0) = F[2] - f_double;
+    const double w0 = leg_des[6] - leg_des[3], w1 = leg_des[7] - leg_des[4], w2 = leg_des[8] - leg_des[5];
+    const double e0 = rfoot_des[0] - leg_des[3], e1 = rfoot_des[1] - leg_des[4], e2 = rfoot_des[2] - leg_des[5];
+    const double rlleg_disx = sqrt(sq(w0) + sq(w1) + sq(w2));
+    const double com_rleg_disx = w0 * e0 + w1 * e1 + w2 * e2;
+    const double rawx = com_rleg_disx / rlleg_disx;
+    const double raw1x = rawx < 1.0 ? rawx : 1.0;
+    const double rleg_comx = raw1x > 0.0 ? raw1x : 0.0;
+    f_double = F[3] * rleg_comx;
+    FRC(0, 2) = f_double;
+    FRC(0, 1) = F[3] - f_double;
+    f_double = F[4] * rleg_comx * y_coefficient;
+    FRC(1, 2) = f_double;
+    FRC(1, 1) = F[4] * y_coefficient - f_double;
+    f_double = F[5] * rleg_comx;
+    FRC(2, 2) = f_double;
+    FRC(2, 1) = F[5] - f_double;
+  }  // other modes: F_leg_ref unchanged (:247-250)
+#undef FRC
+}
+
+__global__ __launch_bounds__(64) void force_qp_kernel(const ForceArgs a) {
+  __shared__ ForceLds S;
+  const int lane = threadIdx.x, grp = lane >> 4, li = lane & 15;
+  const int64_t inst = (int64_t)blockIdx.x * GI_GROUPS + grp;
+  // shared constant rows: qp_H / qp_h (dynmics_compute.cpp:75-98), CI = -qp_H'
+  for (int k = lane; k < 12 * 24; k += 64) S.CI[k] = 0.0;
+  if (lane < 16) S.zeros[lane] = 0.0;
+  __syncthreads();
+  if (lane < 4) {
+    const int i = lane;
+    // CI(v, c) = -qpH(c, v), stored CI[c*12 + v]
+    S.CI[(2 * i) * 12 + 3 * i + 2] = 1.0;          // qpH(2i, 3i+2) = -1
+    S.CI[(2 * i + 1) * 12 + 3 * i + 2] = -1.0;     // qpH(2i+1, 3i+2) = 1
+    S.ci0[2 * i] = 0.0;
+    S.ci0[2 * i + 1] = a.fz_max;
+    S.CI[(8 + 2 * i) * 12 + 3 * i] = 1.0;          // qpH(8+2i, 3i) = -1
+    S.CI[(8 + 2 * i) * 12 + 3 * i + 2] = a.mu;     // qpH(8+2i, 3i+2) = -mu
+    S.CI[(8 + 2 * i + 1) * 12 + 3 * i] = -1.0;
+    S.CI[(8 + 2 * i + 1) * 12 + 3 * i + 2] = a.mu;
+    S.ci0[8 + 2 * i] = 0.0;
+    S.ci0[8 + 2 * i + 1] = 0.0;
+    S.CI[(16 + 2 * i) * 12 + 3 * i + 1] = 1.0;
+    S.CI[(16 + 2 * i) * 12 + 3 * i + 2] = a.mu;
+    S.CI[(16 + 2 * i + 1) * 12 + 3 * i + 1] = -1.0;
+    S.CI[(16 + 2 * i + 1) * 12 + 3 * i + 2] = a.mu;
+    S.ci0[16 + 2 * i] = 0.0;
+    S.ci0[16 + 2 * i + 1] = 0.0;
+  }
+  __syncthreads();
+  if (inst >= a.batch) return;
+  ForceLds::Grp &P = S.g[grp];
+
+  // ---- force_distribution (state F_leg_ref in/out) -> F_leg_guess
+  double Fref[12];
+  for (int k = 0; k < 12; ++k) Fref[k] = a.F_leg_ref[inst * 12 + k];
+  force_distribution(a.com_des + inst * 3, a.leg_des + inst * 12, a.F_force_des + inst * 6,
+                     a.mode[inst], a.y_coef[inst], a.rfoot_des + inst * 3, a.lfoot_des + inst * 3,
+                     Fref);
+  if (li < 12) P.guess[li] = Fref[li];
+  // ---- force_opt: A (6x12, col-major) with the skew_hat quirk (:274-298)
+  if (li < 12) {
+    for (int k = 0; k < 6; ++k) P.A[li * 6 + k] = 0.0;
+  }
+  GI_SYNC();
+  if (li < 4) {
+    const int leg = li;
+    const double *bp = a.base_p + inst * 3;
+    const double *fp = a.feet_p + inst * 12 + 3 * leg;
+    const double v0 = bp[0] - fp[0];  // skew_hat uses vec_w[0] everywhere (comma operator)
+    for (int k = 0; k < 3; ++k) P.A[(3 * leg + k) * 6 + k] = 1.0;
+    // W rows [0,-a,a],[a,0,-a],[-a,a,0]
+    const double W[3][3] = {{0.0, -v0, v0}, {v0, 0.0, -v0}, {-v0, v0, 0.0}};
+    for (int r = 0; r < 3; ++r)
+      for (int k = 0; k < 3; ++k) P.A[(3 * leg + k) * 6 + 3 + r] = W[r][k];
+  }
+  GI_SYNC();
+  // G = 2 (alpha A'A + (beta+gamma) I), then (G' + G)/2 ; g0 (:300-305)
+  double Grow[12];
+  if (li < 12) {
+    const int r = li;
+    for (int c = 0; c < 12; ++c) {
+      double ata = 0.0;
+      for (int k = 0; k < 6; ++k) ata += P.A[r * 6 + k] * P.A[c * 6 + k];
+      Grow[c] = 2.0 * (a.alpha * ata + (r == c ? (a.beta + a.gamma) : 0.0));
+    }
+    for (int c = 0; c < 12; ++c) P.G[c * 12 + r] = Grow[c];  // column-major, entry (r,c)
+  }
+  GI_SYNC();
+  if (li < 12) {
+    const int r = li;
+    for (int c = 0; c < 12; ++c) Grow[c] = (P.G[r * 12 + c] + P.G[c * 12 + r]) / 2.0;
+  }
+  GI_SYNC();
+  if (li < 12) {
+    const int r = li;
+    for (int c = 0; c < 12; ++c) P.G[c * 12 + r] = Grow[c];
+    double atf = 0.0;
+    const double *FT = a.FT_total_des + inst * 6;
+    for (int k = 0; k < 6; ++k) atf += P.A[r * 6 + k] * FT[k];
+    P.g0[r] = -2.0 * (a.alpha * atf + a.beta * P.guess[r] + a.gamma * a.grf_opt[inst * 12 + r]);
+    for (int c = 0; c < 12; ++c) P.CE[c * 12 + r] = 0.0;
+  }
+  GI_SYNC();
+  // swing-leg equality pattern AA (:310-350)
+  if (li == 0) {
+    const int mode = a.mode[inst], rs = a.right_support[inst];
+    int z0 = -1, z1 = -1;
+    if (mode == 102) {
+      if (rs == 0) { z0 = 1; z1 = 2; }
+      else if (rs == 1) { z0 = 0; z1 = 3; }
+    } else if (mode == 101) {
+      if (rs == 0) { z0 = 0; z1 = 2; }
+      else if (rs == 1) { z0 = 1; z1 = 3; }
+    }
+    if (z0 >= 0)
+      for (int k = 0; k < 3; ++k) {
+        P.CE[(3 * z0 + k) * 12 + 3 * z0 + k] = 1.0;
+        P.CE[(3 * z1 + k) * 12 + 3 * z1 + k] = 1.0;
+      }
+  }
+  GI_SYNC();
+  double f;
+  int st, it;
+  gi_solve_group(P.gi, li, 12, 12, 24, P.G, 12, P.g0, P.CE, S.zeros, S.CI, S.ci0, P.x, f, st, it);
+  GI_SYNC();
+  // QPBaseClass::solveQP: success iff no NaN (:200-227); Solve / fallback
+  bool ok = true;
+  for (int k = 0; k < 12; ++k) ok = ok && !isnan(P.x[k]);
+  if (li < 12) {
+    a.grf_opt[inst * 12 + li] = ok ? P.x[li] : P.guess[li];
+    a.F_leg_guess[inst * 12 + li] = P.guess[li];
+    a.F_leg_ref[inst * 12 + li] = Fref[li];
+  }
+  if (li == 0) {
+    if (a.qp_solution) a.qp_solution[inst] = ok ? 1 : 0;
+    if (a.status) a.status[inst] = st;
+    if (a.iters) a.iters[inst] = it;
+  }
+}
+
+// dynmics_compute.cpp:109-138, one thread per (instance, leg)
+__global__ void joint_torque_kernel(int64_t batch, const double *Jaco, const int *swing,
+                                    const double *p_des, const double *p_est,
+                                    const double *pv_des, const double *pv_est,
+                                    const double *F_leg_ref, double *tau) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= batch * 4) return;
+  const int64_t inst = t >> 2;
+  const int leg = (int)(t & 3);
+  const double swing_kp = 1.0, swing_kd = 0.01;             // :37-38
+  const double gcomp = (leg & 1) ? 0.80 : -0.80;            // :39-41 row 0
+  const double *J = Jaco + t * 9;
+  double f[3];
+  if (swing[t]) {
+    for (int k = 0; k < 3; ++k)
+      f[k] = swing_kp * (p_des[t * 3 + k] - p_est[t * 3 + k]) +
+             swing_kd * (pv_des[t * 3 + k] - pv_est[t * 3 + k]);
+  } else {
+    for (int k = 0; k < 3; ++k) f[k] = F_leg_ref[inst * 12 + leg * 3 + k];
+  }
+  for (int r = 0; r < 3; ++r) {
+    double acc = 0.0;
+    for (int k = 0; k < 3; ++k) acc += J[r * 3 + k] * f[k];
+    tau[t * 3 + r] = -acc + (r == 0 ? gcomp : 0.0);
+  }
+}
+
+}  // namespace qloco
+
+using namespace qloco;
+
+extern "C" void qloco_force_params_default(qloco_force_params *p) {
+  p->mass = 12.0;
+  p->alpha = 10000.0;
+  p->beta = 1000.0;
+  p->gamma = 10.0;
+  p->fz_max = 160.0;
+  p->mu = 0.25;
+}
+
+extern "C" int qloco_force_qp_solve(const qloco_force_params *prm, int64_t batch,
+                                    const double *com_des, const double *leg_des,
+                                    const double *F_force_des, const double *rfoot_des,
+                                    const double *lfoot_des, const double *base_p,
+                                    const double *feet_p, const double *FT_total_des,
+                                    const int32_t *mode, const int32_t *right_support,
+                                    const double *y_coef, double *F_leg_ref, double *grf_opt,
+                                    double *F_leg_guess, int32_t *qp_solution, int32_t *status,
+                                    int32_t *iters, void *stream) {
+  if (!prm || batch < 0) return QLOCO_ERR_ARG;
+  if (batch == 0) return QLOCO_OK;
+  if (!com_des || !leg_des || !F_force_des || !rfoot_des || !lfoot_des || !base_p || !feet_p ||
+      !FT_total_des || !mode || !right_support || !y_coef || !F_leg_ref || !grf_opt ||
+      !F_leg_guess)
+    return QLOCO_ERR_ARG;
+  ForceArgs a;
+  memset(&a, 0, sizeof(a));
+  a.mass = prm->mass;
+  a.alpha = prm->alpha;
+  a.beta = prm->beta;
+  a.gamma = prm->gamma;
+  a.fz_max = prm->fz_max;
+  a.mu = prm->mu;
+  a.batch = batch;
+  a.com_des = com_des;
+  a.leg_des = leg_des;
+  a.F_force_des = F_force_des;
+  a.rfoot_des = rfoot_des;
+  a.lfoot_des = lfoot_des;
+  a.base_p = base_p;
+  a.feet_p = feet_p;
+  a.FT_total_des = FT_total_des;
+  a.y_coef = y_coef;
+  a.mode = mode;
+  a.right_support = right_support;
+  a.F_leg_ref = F_leg_ref;
+  a.grf_opt = grf_opt;
+  a.F_leg_guess = F_leg_guess;
+  a.qp_solution = qp_solution;
+  a.status = status;
+  a.iters = iters;
+  const unsigned blocks = (unsigned)((batch + GI_GROUPS - 1) / GI_GROUPS);
+  hipLaunchKernelGGL(force_qp_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+  QLOCO_HIP_CHECK(hipGetLastError(), "force_qp_kernel launch");
+  return QLOCO_OK;
+}
+
+extern "C" int qloco_joint_torques(int64_t batch, const double *Jaco, const int32_t *swing,
+                                   const double *p_des, const double *p_est,
+                                   const double *pv_des, const double *pv_est,
+                                   const double *F_leg_ref, double *tau, void *stream) {
+  if (batch < 0 || (batch > 0 && (!Jaco || !swing || !p_des || !p_est || !pv_des || !pv_est ||
+                                  !F_leg_ref || !tau)))
+    return QLOCO_ERR_ARG;
+  if (batch == 0) return QLOCO_OK;
+  const int64_t threads = batch * 4;
+  hipLaunchKernelGGL(joint_torque_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, batch, Jaco, swing, p_des, p_est, pv_des, pv_est,
+                     F_leg_ref, tau);
+  QLOCO_HIP_CHECK(hipGetLastError(), "joint_torque_kernel launch");
+  return QLOCO_OK;
+}

@@ -924,10 +924,11 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
                                    int32_t *status, int32_t *iters, int32_t *rho_updates,
                                    float *obj, float *warm, int32_t max_stance_legs,
                                    void *stream) {
-  if (!spec || batch < 0 || !x0 || !x_ref || !feet || !contacts || !u0) return QLOCO_ERR_ARG;
+  if (!spec || batch < 0) return QLOCO_ERR_ARG;
   if (spec->horizon < 1 || spec->horizon > kMaxN) return QLOCO_BAD_SIZE;
-  if (spec->warm_start && !warm) return QLOCO_ERR_ARG;
   if (batch == 0) return QLOCO_OK;
+  if (!x0 || !x_ref || !feet || !contacts || !u0) return QLOCO_ERR_ARG;
+  if (spec->warm_start && !warm) return QLOCO_ERR_ARG;
   SrbdArgs a;
   memset(&a, 0, sizeof(a));
   a.N = spec->horizon;

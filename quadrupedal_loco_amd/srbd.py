@@ -60,14 +60,21 @@ class SrbdResult:
 
 
 def max_stance_legs(contacts, horizon, contacts_per_step=True):
-    """Largest number of stance (step, leg) pairs in the batch (host sync)."""
-    if contacts_per_step:
-        return int(contacts.reshape(contacts.shape[0], -1).sum(dim=1).max().item()) \
-            if hasattr(contacts, "sum") and hasattr(contacts, "device") else \
-            int(np.asarray(contacts).reshape(len(contacts), -1).sum(axis=1).max())
-    per = contacts.reshape(contacts.shape[0], 4).sum(dim=1).max().item() \
-        if hasattr(contacts, "device") else np.asarray(contacts).reshape(-1, 4).sum(1).max()
-    return int(per) * horizon
+    """Largest number of stance (step, leg) pairs in the batch (host sync for tensors)."""
+    try:
+        import torch
+        is_t = isinstance(contacts, torch.Tensor)
+    except ImportError:  # pragma: no cover
+        is_t = False
+    if len(contacts) == 0:
+        return 0
+    if is_t:
+        c = contacts.reshape(contacts.shape[0], -1).to(torch.int32)
+        per = int(c.sum(dim=1).max().item())
+    else:
+        c = np.asarray(contacts).reshape(len(contacts), -1).astype(np.int64)
+        per = int(c.sum(axis=1).max())
+    return per if contacts_per_step else per * horizon
 
 
 class BatchedConvexMpc:
