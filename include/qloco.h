@@ -102,6 +102,18 @@ int qloco_srbd_solve(const qloco_srbd_spec *spec, int64_t batch, const float *x0
                      float *u0, float *u, int32_t *status, int32_t *iters, float *obj,
                      float *warm, void *stream);
 
+/* Extended form of qloco_srbd_solve: additionally returns rho_updates[B]
+ * (number of adaptive-rho refactorisations) and takes max_stance_legs, the
+ * largest number of stance (step, leg) pairs of any instance in the batch
+ * (<= 21 selects the one-wavefront kernel, <= 42 the two-wavefront one;
+ * 0 = assume the worst case 4N).  An instance with more stance pairs than
+ * the selected kernel holds gets status QLOCO_BAD_SIZE and NaN forces. */
+int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, const float *x0,
+                        const float *x_ref, const float *feet, const uint8_t *contacts,
+                        float *u0, float *u, int32_t *status, int32_t *iters,
+                        int32_t *rho_updates, float *obj, float *warm,
+                        int32_t max_stance_legs, void *stream);
+
 /* Batched condensed-QP build only (ConvexMpc::calculate_qp_mats, dense,
  * as the reference materialises it).  Outputs per instance (NULL = skip):
  *   H[B*(12N)^2] col-major, g[B*12N], lb[B*20N], ub[B*20N] (+-1e30 = INFTY),

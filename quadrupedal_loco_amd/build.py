@@ -21,6 +21,7 @@ ARCH = "gfx950"
 SOURCES = [
     "qloco_capi.hip",
     "qloco_srbd.hip",
+    "qloco_srbd_build.hip",
     "qloco_gi.hip",
     "qloco_force.hip",
     "qloco_body.hip",
@@ -28,8 +29,12 @@ SOURCES = [
 ]
 # per-file extra flags: the fp64 active-set kernel keeps the restatement's
 # exact operation sequence (no FMA contraction)
+# The SRBD kernel keeps a 64-wide register row per lane: SLP vectorisation
+# pairs unrelated columns across the unrolled row loops and inflates live
+# ranges into scratch spills, so it is off there (the packed-fp32 matvec and
+# Gauss-Jordan updates are written with explicit float2 ops).
 EXTRA = {"qloco_gi.hip": ["-ffp-contract=off"], "qloco_force.hip": ["-ffp-contract=off"],
-         "qloco_body.hip": ["-ffp-contract=off"]}
+         "qloco_body.hip": ["-ffp-contract=off"], "qloco_srbd.hip": ["-fno-slp-vectorize"]}
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC]
 

@@ -16,16 +16,19 @@
 //    block is b + (i-j) e with b (rows 6..11) and e (rows 0..5) disjoint:
 //    H[r][c] = K0(j_r,j_c) * <b_r,b_c>_Q + K2(j_r,j_c) * <e_r,e_c>_Q + R,
 //    K0 = #{i >= max(j_r,j_c)}, K2 = sum_i (i-j_r)(i-j_c).  Bqp x and
-//    Bqp' w (gradient, dual residual) are prefix/suffix sums over steps.
+//    Bqp' w (gradient, P x for the residuals) are per-step prefix / suffix
+//    sums computed by all lanes in parallel.
 //  * ADMM is OSQP's algorithm (Ruiz scaling, rho vector, relaxation,
 //    termination every check_termination iterations, adaptive rho) in fp32.
 //    Lane v owns stance variable v (leg triples never straddle a wave:
-//    21 legs = 63 lanes per wave, lane 63 idles), its row of K^-1 in VGPRs
-//    (K = P + sigma I + A' diag(rho) A, inverted by Gauss-Jordan with a
-//    wave-uniform pivot index -> s_set_gpr_idx, no scratch), and the <= 2
-//    constraint rows of its leg's 5 (x: rows 0,1; y: rows 2,3; z: row 4).
+//    21 legs = 63 lanes per wave, lane 63 pads), its row of K^-1 in 32*W
+//    packed-fp32 VGPR pairs (K = P + sigma I + A' diag(rho) A, inverted in
+//    place by Gauss-Jordan), and the <= 2 constraint rows of its leg's 5
+//    (x: rows 0,1; y: rows 2,3; z: row 4).  Padding rows/columns are the
+//    identity, so every loop over columns is straight-line code.
 //    Per iteration: one LDS broadcast of the KKT right-hand side, one
-//    64-wide matvec against the register-resident K^-1, three lane shuffles.
+//    packed-FMA matvec against the register-resident K^-1, four DPP lane
+//    shifts (wave_shr/wave_shl) for the leg-local constraint couplings.
 #include <math.h>
 #include <string.h>
 
@@ -54,433 +57,379 @@ struct SrbdArgs {
   int *status, *iters, *rho_updates;
 };
 
-typedef float v32f __attribute__((ext_vector_type(32)));
 typedef float f2v __attribute__((ext_vector_type(2)));
-typedef float f8v __attribute__((ext_vector_type(8)));
-typedef float f16v __attribute__((ext_vector_type(16)));
-typedef int i2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
 
-// One register row of K / K^-1: separate vector members (never an array of
-// vectors) and no dynamically-indexed element stores, so SROA keeps the row
-// in VGPRs; dynamic (wave-uniform) element reads lower to s_set_gpr_idx.
+// One register row of K / K^-1 as packed pairs; every index is static after
+// unrolling, so SROA keeps it in VGPRs.
 template <int W>
-struct Row;
-template <>
-struct Row<1> {
-  v32f k0, k1;
-  __device__ __forceinline__ float get(int c) const {
-    const int e = c & 31;
-    const float a0 = k0[e], a1 = k1[e];
-    return (c >> 5) == 0 ? a0 : a1;
-  }
-  __device__ __forceinline__ void set(int c, float x) {
-    if ((c >> 5) == 0) k0[c & 31] = x;
-    else k1[c & 31] = x;
-  }
-  __device__ __forceinline__ void scale(float s) { k0 *= s; k1 *= s; }
-  __device__ __forceinline__ void zero() { k0 = (v32f)(0.0f); k1 = (v32f)(0.0f); }
+struct Row {
+  f2v k[32 * W];
 };
-template <>
-struct Row<2> {
-  v32f k0, k1, k2, k3;
-  __device__ __forceinline__ float get(int c) const {
-    const int ch = c >> 5, e = c & 31;
-    const float a0 = k0[e], a1 = k1[e], a2 = k2[e], a3 = k3[e];
-    return ch == 0 ? a0 : (ch == 1 ? a1 : (ch == 2 ? a2 : a3));
-  }
-  __device__ __forceinline__ void set(int c, float x) {
-    const int ch = c >> 5, e = c & 31;
-    if (ch == 0) k0[e] = x;
-    else if (ch == 1) k1[e] = x;
-    else if (ch == 2) k2[e] = x;
-    else k3[e] = x;
-  }
-  __device__ __forceinline__ void scale(float s) { k0 *= s; k1 *= s; k2 *= s; k3 *= s; }
-  __device__ __forceinline__ void zero() {
-    k0 = (v32f)(0.0f); k1 = (v32f)(0.0f); k2 = (v32f)(0.0f); k3 = (v32f)(0.0f);
-  }
-};
+#define KE(K, c) ((K).k[(c) >> 1][(c)&1])
 
 template <int W>
 struct SrbdLds {
-  static constexpr int NC = 64 * W;  // register-row length (columns)
+  static constexpr int NC = 64 * W;
+  f4v bc[2][NC / 4];       // broadcast ring (KKT rhs, GJ pivot rows, Ruiz D)
+  f4v bv[NC][2];           // per var: {b0,b1,b2,e0}, {e1,e2,step,comp}
+  float xs[NC];            // unscaled x per var (P x)
+  float Dc[NC];            // Ruiz column scaling D
+  float err[12 * kMaxN];   // per-step row values (gradient error / aggregates)
+  float Wc[12 * kMaxN];    // per-step Bqp' weights: rows 0..5 W1, rows 6..11 W0
+  float q2[16];
+  float r2[12];
   float x0[16];
-  float err[13 * kMaxN];     // scratch for gradient / P x
-  float W0[13 * kMaxN];      // suffix sums  sum_{i>=j} w_i
-  float W1[13 * kMaxN];      //              sum_{i>=j} (i-j) w_i
-  float agg[12 * kMaxN];     // per-step aggregates of coef * x
-  float bv[NC][8];           // per var: coef b(6..8), e(0..2), step, comp
-  float bc[2][NC];           // broadcast ring (matvec rhs, pivots, D)
-  float xs[NC];              // unscaled x per var (for P x)
-  float piv[2];              // pivot values of the GJ ring
-  float red[W][16];          // cross-wave reduction slots
-  int legtab[4 * kMaxN];     // stance pair -> 4*step + leg
-  int stepstart[kMaxN + 1];  // first stance pair of each step
-  uint8_t ct[4 * kMaxN];
+  float aux[3][NC];         // per var, read off the hot path: 2 r (R diag), E row0, E row1
+  int pair[NC];             // per var: 4*step + leg
+  float piv[2];
+  float red[W][16];
+  int legtab[4 * kMaxN];   // stance pair -> 4*step + leg
+  int stepstart[kMaxN + 1];
   int nlegs;
+  uint8_t ct[4 * kMaxN];
 };
 
-// K0 / K2 horizon sums for the closed-form Hessian (see header comment)
-__device__ __forceinline__ void k0k2(int ja, int jb, int N, float &K0, float &K2) {
-  int M = ja > jb ? ja : jb;
-  int T = N - M;
-  int al = M - ja, be = M - jb;
-  int S1 = T * (T - 1) / 2;
-  int S2 = (T - 1) * T * (2 * T - 1) / 6;
-  K0 = (float)T;
-  K2 = (float)(S2 + (al + be) * S1 + al * be * T);
+// LDS ordering between the lanes of ONE wave needs no s_barrier (a wave's
+// LDS instructions execute in order); only the compiler must not move
+// memory operations across the point.
+template <int W>
+__device__ __forceinline__ void bsync() {
+  if constexpr (W == 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
 }
 
-// Block-wide max/sum of NVAL values (all threads get the result).
-template <int W, int NVAL>
-__device__ __forceinline__ void block_reduce(float (&v)[NVAL], const bool (&is_sum)[NVAL],
-                                             float (*red)[16]) {
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF,
+                                                            0xF, false));
+}
+__device__ __forceinline__ float lane_prev(float v) { return dpp<0x138>(v); }  // wave_shr:1
+__device__ __forceinline__ float lane_next(float v) { return dpp<0x130>(v); }  // wave_shl:1
+__device__ __forceinline__ float rlane(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+// Wave-uniform max / sum over 64 lanes: DPP within 16-lane rows, then the
+// four row results combined in a fixed order (deterministic).
+__device__ __forceinline__ float wmax(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dpp<0x124>(v));  // row_ror:4
+  v = fmaxf(v, dpp<0x128>(v));  // row_ror:8
+  return fmaxf(fmaxf(rlane(v, 0), rlane(v, 16)), fmaxf(rlane(v, 32), rlane(v, 48)));
+}
+__device__ __forceinline__ float wsum(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x124>(v);
+  v += dpp<0x128>(v);
+  return (rlane(v, 0) + rlane(v, 16)) + (rlane(v, 32) + rlane(v, 48));
+}
+
+// Block-wide reductions (wave-uniform results).
+template <int W, int NV>
+__device__ __forceinline__ void bmax(float (&v)[NV], float (*red)[16]) {
 #pragma unroll
-  for (int k = 0; k < NVAL; ++k) v[k] = is_sum[k] ? wave_sum(v[k]) : wave_max(v[k]);
-  if (W > 1) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) {
+  for (int k = 0; k < NV; ++k) v[k] = wmax(v[k]);
+  if constexpr (W > 1) {
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
 #pragma unroll
-      for (int k = 0; k < NVAL; ++k) red[wave][k] = v[k];
-    }
+      for (int k = 0; k < NV; ++k) red[wave][k] = v[k];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < NVAL; ++k) {
+    for (int k = 0; k < NV; ++k) {
       float r = red[0][k];
 #pragma unroll
-      for (int w = 1; w < W; ++w) r = is_sum[k] ? (r + red[w][k]) : fmaxf(r, red[w][k]);
-      v[k] = r;
+      for (int w = 1; w < W; ++w) r = fmaxf(r, red[w][k]);
+      v[k] = uni(r);
     }
     __syncthreads();
   }
-#pragma unroll
-  for (int k = 0; k < NVAL; ++k) v[k] = uni(v[k]);
 }
-
-// coefficient of stance variable (bv entry) on condensed-state row s (0..11)
-__device__ __forceinline__ float coef_row(const float *bvc, int s, float dtm, float dt2m) {
-  const int comp = (int)bvc[7];
-  if (s < 3) return bvc[3 + s];
-  if (s < 6) return (comp == s - 3) ? dt2m : 0.0f;
-  if (s < 9) return bvc[s - 6];
-  return (comp == s - 9) ? dtm : 0.0f;
-}
-
-// Suffix sums of (Bqp' w): given err/w in S.err[13*i + s] (rows 0..11),
-// write W0[13*j + s] = sum_{i>=j} w_i[s], W1 = sum_{i>=j} (i-j) w_i[s].
 template <int W>
-__device__ __forceinline__ void suffix_sums(SrbdLds<W> &S, int N) {
-  const int t = threadIdx.x;
-  if (t < 12) {
-    float a0 = 0.0f, a1 = 0.0f;
-    for (int i = N - 1; i >= 0; --i) {
-      a1 += a0;
-      a0 += S.err[13 * i + t];
-      S.W0[13 * i + t] = a0;
-      S.W1[13 * i + t] = a1;
-    }
+__device__ __forceinline__ float bsum(float v, float (*red)[16]) {
+  v = wsum(v);
+  if constexpr (W > 1) {
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[wave][15] = v;
+    __syncthreads();
+    float r = red[0][15];
+#pragma unroll
+    for (int w = 1; w < W; ++w) r += red[w][15];
+    v = uni(r);
+    __syncthreads();
   }
+  return v;
 }
 
-// (Bqp' w)_v for this lane's variable from W0/W1 of its step.
-__device__ __forceinline__ float bqp_t_w(const float *W0, const float *W1, int step,
-                                         const f8v bvr, float dtm, float dt2m) {
-  const int comp = (int)bvr[7];
-  const float *w0 = W0 + 13 * step, *w1 = W1 + 13 * step;
-  float acc = bvr[0] * w0[6] + bvr[1] * w0[7] + bvr[2] * w0[8];
-  acc += dtm * w0[9 + comp];
-  acc += bvr[3] * w1[0] + bvr[4] * w1[1] + bvr[5] * w1[2];
-  acc += dt2m * w1[3 + comp];
+// (Bqp' w)_v for a variable of step `step`, component `comp`, from S.Wc.
+template <int W>
+__device__ __forceinline__ float bqp_t(const SrbdLds<W> &S, int step, int comp, f4v lo, f4v hi,
+                                       float dtm, float dt2m) {
+  const float *w = S.Wc + 12 * step;
+  float acc = lo.x * w[6] + lo.y * w[7] + lo.z * w[8];
+  acc += lo.w * w[0] + hi.x * w[1] + hi.y * w[2];
+  acc += dtm * w[9 + comp] + dt2m * w[3 + comp];
   return acc;
 }
 
-// Unscaled P x (P = Bqp' Q Bqp + R) for this lane's variable.  S.xs holds
-// the unscaled x of every variable.  Four barriers.
+// S.Wc[j][r] = sum_{i>=j} wt(i-j) S.err[i][r]; wt = 1 on b rows (6..11,
+// W0), (i-j) on e rows (0..5, W1).  Parallel over (j, r).
 template <int W>
-__device__ __forceinline__ float p_times_x(SrbdLds<W> &S, const SrbdArgs &a, int N, int nvalid, bool valid,
-                           int step, const f8v bvr, float r2v, float xv, float dtm,
-                           float dt2m) {
+__device__ __forceinline__ void suffix_weights(SrbdLds<W> &S, int N) {
+  for (int idx = threadIdx.x; idx < 12 * N; idx += 64 * W) {
+    const int j = idx / 12, r = idx - 12 * j;
+    const bool brow = r >= 6;
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < kMaxN; ++i) {
+      if (i < N) {
+        const float e = S.err[12 * i + r];
+        const float wt = (i >= j) ? (brow ? 1.0f : (float)(i - j)) : 0.0f;
+        acc = fmaf(wt, e, acc);
+      }
+    }
+    S.Wc[idx] = acc;
+  }
+}
+
+// Unscaled (P x)_v, P = Bqp' Q Bqp + R.  Caller has written S.xs (unscaled
+// x, 0 on padding) and synced.  Three phases, all lanes busy:
+//  (a) per-step aggregates agg_j[s] = sum_{v in step j} Bcoef(v, s) x_v
+//  (b) state rows s_i (b rows: prefix sum, e rows: weighted prefix sum),
+//      w_i = Q s_i, suffix weights W0 / W1 per (j, r) -> S.Wc
+//  (c) this lane's (Bqp' w)_v + R x_v
+template <int W>
+__device__ __forceinline__ float p_times_x(SrbdLds<W> &S, int N, bool valid, int step, int comp,
+                                           f4v lo, f4v hi, float r2v, float xu, float dtm,
+                                           float dt2m) {
   const int t = threadIdx.x;
-  // (a) per-step aggregates agg_j[s] = sum_{v in step j} coef(v, s) x_v
   for (int idx = t; idx < 12 * N; idx += 64 * W) {
     const int j = idx / 12, s = idx - 12 * j;
+    const int sg = s / 3, sc = s - 3 * sg;  // 0: e rows, 1: p rows, 2: b rows, 3: v rows
+    const int off = (sg == 0 ? 3 : 0) + sc;
+    const float dsc = sg == 1 ? dt2m : dtm;
+    const int p0 = S.stepstart[j], p1 = S.stepstart[j + 1];
     float acc = 0.0f;
-    for (int p = S.stepstart[j]; p < S.stepstart[j + 1]; ++p) {
-      const int vb = 64 * (p / kLegsPerWave) + 3 * (p % kLegsPerWave);
 #pragma unroll
-      for (int c = 0; c < 3; ++c) acc += coef_row(S.bv[vb + c], s, dtm, dt2m) * S.xs[vb + c];
+    for (int q = 0; q < 4; ++q) {
+      const int p = p0 + q;
+      if (p < p1) {
+        const int vb = 64 * (p / kLegsPerWave) + 3 * (p % kLegsPerWave);
+        const float *bf = reinterpret_cast<const float *>(&S.bv[vb][0]);
+        const float xa = S.xs[vb], xb = S.xs[vb + 1], xc = S.xs[vb + 2];
+        const float ev = bf[off] * xa + bf[8 + off] * xb + bf[16 + off] * xc;
+        const float xsel = sc == 0 ? xa : (sc == 1 ? xb : xc);
+        acc += (sg & 1) ? dsc * xsel : ev;
+      }
     }
-    S.agg[idx] = acc;
+    S.err[idx] = acc;
   }
-  __syncthreads();
-  // (b) state trajectory s_i = sum_{j<=i} [B rows: agg_j ; E rows: (i-j) agg_j],
-  //     w_i = Q s_i, then suffix sums (same lane owns one row s throughout)
-  if (t < 12) {
-    float pa = 0.0f, pe = 0.0f, s1 = 0.0f;
-    const bool brow = t >= 6;
-    for (int i = 0; i < N; ++i) {
-      const float ag = S.agg[12 * i + t];
-      s1 += pe;  // sum_{j<i} agg_j accumulated (i-j) times
-      pe += ag;
-      pa += ag;
-      const float si = brow ? pa : s1;
-      S.err[13 * i + t] = a.q2[t] * si;
+  bsync<W>();
+  for (int idx = t; idx < 12 * N; idx += 64 * W) {
+    const int jv = idx / 12, r = idx - 12 * jv;
+    const bool brow = r >= 6;
+    float pa = 0.0f, pe = 0.0f, se = 0.0f, acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < kMaxN; ++i) {
+      if (i < N) {
+        const float ag = S.err[12 * i + r];
+        se += pe;  // sum_{j<i} (i-j) agg_j
+        pe += ag;
+        pa += ag;
+        const float si = brow ? pa : se;
+        const float wt = (i >= jv) ? (brow ? 1.0f : (float)(i - jv)) : 0.0f;
+        acc = fmaf(wt, si, acc);
+      }
     }
+    S.Wc[idx] = S.q2[r] * acc;
   }
-  suffix_sums<W>(S, N);
-  __syncthreads();
-  float px = 0.0f;
-  if (valid) px = bqp_t_w(S.W0, S.W1, step, bvr, dtm, dt2m) + r2v * xv;
-  __syncthreads();
-  (void)nvalid;
-  return px;
+  bsync<W>();
+  return valid ? bqp_t<W>(S, step, comp, lo, hi, dtm, dt2m) + r2v * xu : 0.0f;
 }
 
-// Per-lane state of one stance variable and its owned constraint rows.
-struct LaneVar {
-  int t, lane, comp, step, leg, nrow, zl;
-  bool valid;
-  f8v bvr;
-  float r2v, bq0, bq1, bq2, eq0, eq1, eq2, linb, line;
-  f2v ra, rz, rl, ru, rE, Einv, lh, uh, rv;
-  i2v ctype;
-  float Dr, Dinv, cs, cinv, qv;
-  float x;
-  f2v zr, yr;
-};
+// K0 / K2 horizon sums (exact small integers in fp32).
+__device__ __forceinline__ void k0k2(float ja, float jb, float Nf, float &K0, float &K2) {
+  const float M = fmaxf(ja, jb);
+  const float T = Nf - M;
+  const float al = M - ja, be = M - jb;
+  const float S1 = 0.5f * T * (T - 1.0f);
+  const float S2 = rintf(S1 * (2.0f * T - 1.0f) * (1.0f / 3.0f));
+  K0 = T;
+  K2 = S2 + (al + be) * S1 + al * be * T;
+}
 
-template <int W>
-struct ColMask {
-  int wcols[W];
-  __device__ __forceinline__ bool ok(int c0) const { return (c0 & 63) < wcols[c0 >> 6]; }
+// This lane's coefficients for the closed-form P row.
+struct PCoef {
+  float bq0, bq1, bq2, eq0, eq1, eq2, linb, line;
 };
-
-// Unscaled condensed-Hessian row (closed form), identity on padding lanes.
 template <int W>
-__device__ __forceinline__ void gen_p_row(const SrbdLds<W> &S, const LaneVar &v, int N,
-                                          const ColMask<W> &cm, Row<W> &K) {
+__device__ __forceinline__ PCoef p_coef(const SrbdLds<W> &S, f4v lo, f4v hi, int comp, bool valid,
+                                        float dtm, float dt2m) {
+  PCoef c;
+  c.bq0 = S.q2[6] * lo.x;
+  c.bq1 = S.q2[7] * lo.y;
+  c.bq2 = S.q2[8] * lo.z;
+  c.eq0 = S.q2[0] * lo.w;
+  c.eq1 = S.q2[1] * hi.x;
+  c.eq2 = S.q2[2] * hi.y;
+  c.linb = valid ? S.q2[9 + comp] * dtm * dtm : 0.0f;
+  c.line = valid ? S.q2[3 + comp] * dt2m * dt2m : 0.0f;
+  return c;
+}
+
+// Row of K = rs * D_c * P_rc + [leg block] (SCALED), or the unscaled P row
+// (!SCALED: rs = 1, D = 1, no leg block).  Padding rows are the identity.
+// Returns the diagonal entry (pivot tracking of invert()).
+template <int W, bool SCALED>
+__device__ __forceinline__ float gen_row(const SrbdLds<W> &S, const PCoef &pc, int t, bool valid,
+                                         int step, int comp, float Nf, float r2v, float rs,
+                                         float add0, float add1, float add2, Row<W> &K) {
   constexpr int NC = 64 * W;
-  // opaque copies: keep LICM from hoisting 64 per-column masks / LDS loads
-  // out of the ADMM loop (that would blow the VGPR budget)
-  int tt = v.t, st = v.step, cp = v.comp;
-  asm volatile("" : "+v"(tt), "+v"(st), "+v"(cp)::"memory");
-  K.zero();
+  // opaque copies: keep LICM from hoisting per-column selects out of the ADMM loop
+  int tt = t, cb = t - comp, cp = comp;
+  float stf = (float)step;
+  asm volatile("" : "+v"(tt), "+v"(cb), "+v"(cp), "+v"(stf));
+  float diag = 1.0f;
 #pragma unroll
-  for (int c0 = 0; c0 < NC; c0 += 4) {
-    if (!cm.ok(c0)) continue;
+  for (int c4 = 0; c4 < NC; c4 += 4) {
+    f4v d4 = (f4v)(1.0f);
+    __builtin_amdgcn_sched_barrier(0);  // bound live ranges: one 4-column group at a time
+    if constexpr (SCALED) d4 = *reinterpret_cast<const f4v *>(&S.Dc[c4]);
 #pragma unroll
     for (int cc = 0; cc < 4; ++cc) {
-      const int c = c0 + cc;
-      const float4 lo = *reinterpret_cast<const float4 *>(&S.bv[c][0]);
-      const float4 hi = *reinterpret_cast<const float4 *>(&S.bv[c][4]);
+      const int c = c4 + cc;
+      const f4v lo = S.bv[c][0], hi = S.bv[c][1];
       float K0, K2;
-      k0k2(st, (int)hi.z, N, K0, K2);
-      const bool same = (cp == (int)hi.w);
-      const float beta = v.bq0 * lo.x + v.bq1 * lo.y + v.bq2 * lo.z + (same ? v.linb : 0.0f);
-      const float epsv = v.eq0 * lo.w + v.eq1 * hi.x + v.eq2 * hi.y + (same ? v.line : 0.0f);
+      k0k2(stf, hi.z, Nf, K0, K2);
+      const bool same = (float)cp == hi.w;
+      const float beta = pc.bq0 * lo.x + pc.bq1 * lo.y + pc.bq2 * lo.z + (same ? pc.linb : 0.0f);
+      const float epsv = pc.eq0 * lo.w + pc.eq1 * hi.x + pc.eq2 * hi.y + (same ? pc.line : 0.0f);
       float pv = K0 * beta + K2 * epsv;
-      pv += (c == tt) ? v.r2v : 0.0f;
-      K.set(c, v.valid ? pv : 0.0f);
+      pv += (c == tt) ? r2v : 0.0f;
+      if constexpr (SCALED) {
+        const int off = c - cb;
+        float ad = off == 0 ? add0 : 0.0f;
+        ad = off == 1 ? add1 : ad;
+        ad = off == 2 ? add2 : ad;
+        pv = fmaf(pv, rs * d4[cc], ad);
+      }
+      pv = valid ? pv : ((c == tt) ? 1.0f : 0.0f);
+      diag = (c == tt) ? pv : diag;
+      KE(K, c) = pv;
     }
   }
-}
-
-// P <- cs * D P D with the final Ruiz scaling (D of every column in bc[0]).
-template <int W>
-__device__ __forceinline__ void scale_p_row(SrbdLds<W> &S, const LaneVar &v,
-                                            const ColMask<W> &cm, Row<W> &K) {
-  constexpr int NC = 64 * W;
-  S.bc[0][v.t] = v.Dr;
-  __syncthreads();
-  const float sr = v.cs * v.Dr;
-#pragma unroll
-  for (int c0 = 0; c0 < NC; c0 += 4) {
-    if (!cm.ok(c0)) continue;
-    const float4 d4 = *reinterpret_cast<const float4 *>(&S.bc[0][c0]);
-    K.set(c0 + 0, K.get(c0 + 0) * (sr * d4.x));
-    K.set(c0 + 1, K.get(c0 + 1) * (sr * d4.y));
-    K.set(c0 + 2, K.get(c0 + 2) * (sr * d4.z));
-    K.set(c0 + 3, K.get(c0 + 3) * (sr * d4.w));
-  }
-  __syncthreads();
-}
-
-// K += sigma I + A' diag(rho) A  (leg-local 3x3 block)
-template <int W>
-__device__ __forceinline__ void add_leg_block(const LaneVar &v, float sigma,
-                                              const ColMask<W> &cm, Row<W> &K) {
-  constexpr int NC = 64 * W;
-  const float d_own = v.rv[0] * v.ra[0] * v.ra[0] + v.rv[1] * v.ra[1] * v.ra[1];
-  const float d_oz = v.rv[0] * v.ra[0] * v.rz[0] + v.rv[1] * v.ra[1] * v.rz[1];
-  const float d_zz = v.rv[0] * v.rz[0] * v.rz[0] + v.rv[1] * v.rz[1] * v.rz[1];
-  const int l1 = (v.lane + 63) & 63, l2 = (v.lane + 62) & 63;
-  const float oz1 = __shfl(d_oz, l1, 64), oz2 = __shfl(d_oz, l2, 64);
-  const float zz1 = __shfl(d_zz, l1, 64), zz2 = __shfl(d_zz, l2, 64);
-  float add0, add1, add2;
-  if (v.comp == 0) {
-    add0 = d_own + sigma; add1 = 0.0f; add2 = d_oz;
-  } else if (v.comp == 1) {
-    add0 = 0.0f; add1 = d_own + sigma; add2 = d_oz;
-  } else {
-    add0 = oz2; add1 = oz1; add2 = d_own + zz1 + zz2 + sigma;
-  }
-  if (!v.valid) { add0 = add1 = add2 = 0.0f; }
-  int c_base = v.t - v.comp;
-  asm volatile("" : "+v"(c_base)::"memory");
-#pragma unroll
-  for (int c0 = 0; c0 < NC; c0 += 4) {
-    if (!cm.ok(c0)) continue;
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-      const int c = c0 + cc;
-      const int off = c - c_base;
-      float a = (off == 0) ? add0 : 0.0f;
-      a = (off == 1) ? add1 : a;
-      a = (off == 2) ? add2 : a;
-      K.set(c, K.get(c) + (a));
-    }
-  }
+  return diag;
 }
 
 // In-place Gauss-Jordan inverse of the register-resident SPD K (no
 // pivoting; Ruiz-scaled, so pivots are O(1)).  Row k is broadcast through
-// LDS with entry k replaced by p+1 and p in a side slot.  With
-// g = A_rk / p (g = 1 - 1/p on the pivot lane) ONE shared update
+// LDS with entry k replaced by p+1 (p = pivot, tracked per lane in `diag`
+// with the same fma the row update performs).  With g = A_rk / p
+// (g = 1 - 1/p on the pivot lane) ONE shared update
 //   A_rc <- A_rc - g * bcast_c
 // performs the whole GJ step, column k included (non-pivot:
-// A_rk - g(p+1) = -g; pivot: p - (1-1/p)(p+1) = 1/p).  A_rk itself is read
-// from the broadcast row: GJ on a symmetric matrix keeps
-// A_rk = +A_kr for unprocessed r and -A_kr for processed r (< k).  No
-// register is ever indexed dynamically, so the row stays in VGPRs.
+// A_rk - g(p+1) = -g; pivot: p - (1-1/p)(p+1) = 1/p).  A_rk is read from the
+// broadcast row: GJ on a symmetric matrix keeps A_rk = +A_kr for
+// unprocessed r and -A_kr for processed r (< k).  Only the n valid pivots
+// run; padding rows/columns are identity and never change.
 template <int W>
-__device__ __forceinline__ void invert(SrbdLds<W> &S, int t, const ColMask<W> &cm,
+__device__ __forceinline__ void invert(SrbdLds<W> &S, int t, const int (&ncol)[W], float diag,
                                        Row<W> &K) {
-  constexpr int NC = 64 * W;
+  constexpr int NQ = 16 * W;
+  float *bcf0 = reinterpret_cast<float *>(&S.bc[0][0]);
+  float *bcf1 = reinterpret_cast<float *>(&S.bc[1][0]);
 #pragma unroll
   for (int w = 0; w < W; ++w) {
-    for (int kk = 0; kk < cm.wcols[w]; ++kk) {
+    for (int kk = 0; kk < ncol[w]; ++kk) {
       const int k = 64 * w + kk;
       const int buf = kk & 1;
+      float *bcf = buf ? bcf1 : bcf0;
       const bool mine = (t == k);
       if (mine) {
 #pragma unroll
-        for (int c0 = 0; c0 < NC; c0 += 4) {
-          if (!cm.ok(c0)) continue;
-          float4 v4;
-          v4.x = K.get(c0 + 0);
-          v4.y = K.get(c0 + 1);
-          v4.z = K.get(c0 + 2);
-          v4.w = K.get(c0 + 3);
-          *reinterpret_cast<float4 *>(&S.bc[buf][c0]) = v4;
+        for (int q = 0; q < NQ; ++q) {
+          const f2v a = K.k[2 * q], b2 = K.k[2 * q + 1];
+          S.bc[buf][q] = (f4v){a.x, a.y, b2.x, b2.y};
         }
-        const float p = S.bc[buf][k];
-        S.piv[buf] = p;
-        S.bc[buf][k] = p + 1.0f;
+        bcf[k] = diag + 1.0f;
+        S.piv[buf] = diag;
       }
-      __syncthreads();
+      bsync<W>();
       const float p = S.piv[buf];
-      const float pinv = 1.0f / p;
-      const float akr = S.bc[buf][t];
+      const float pinv = __builtin_amdgcn_rcpf(p);
+      const float akr = bcf[t];
       const float ak = (t < k) ? -akr : akr;
       const float g = mine ? (1.0f - pinv) : ak * pinv;
+      const f2v ng = (f2v)(-g);
 #pragma unroll
-      for (int c0 = 0; c0 < NC; c0 += 4) {
-        if (!cm.ok(c0)) continue;
-        const float4 p4 = *reinterpret_cast<const float4 *>(&S.bc[buf][c0]);
-        K.set(c0 + 0, fmaf(-g, p4.x, K.get(c0 + 0)));
-        K.set(c0 + 1, fmaf(-g, p4.y, K.get(c0 + 1)));
-        K.set(c0 + 2, fmaf(-g, p4.z, K.get(c0 + 2)));
-        K.set(c0 + 3, fmaf(-g, p4.w, K.get(c0 + 3)));
+      for (int q = 0; q < NQ; ++q) {
+        if ((q & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+        const f4v r4 = S.bc[buf][q];
+        K.k[2 * q] = __builtin_elementwise_fma(ng, (f2v){r4.x, r4.y}, K.k[2 * q]);
+        K.k[2 * q + 1] = __builtin_elementwise_fma(ng, (f2v){r4.z, r4.w}, K.k[2 * q + 1]);
       }
+      diag = fmaf(-g, akr, diag);
     }
   }
-  __syncthreads();
-}
-
-// OSQP update_info: residual norms (all threads participate).
-//  o[0] ||E^-1(Ax-z)||  o[1] ||E^-1 z||  o[2] ||E^-1 A x||  o[3] ||D^-1 rd||
-//  o[4] ||D^-1 q||  o[5] ||D^-1 A'y||  o[6] ||D^-1 P x||  o[7..13] scaled
-//  versions of (Ax-z, z, Ax, rd, q, A'y, Px) for the rho estimate.
-template <int W>
-__device__ __forceinline__ void residuals(SrbdLds<W> &S, const SrbdArgs &a, const LaneVar &v,
-                                          int N, float dtm, float dt2m, float (&o)[14],
-                                          float &px_out) {
-  S.xs[v.t] = v.valid ? v.x * v.Dr : 0.0f;
-  __syncthreads();
-  const float pxo = p_times_x<W>(S, a, N, 0, v.valid, v.step, v.bvr, v.r2v, S.xs[v.t], dtm, dt2m);
-  const float pxh = v.cs * v.Dr * pxo;
-  px_out = pxh;
-  const float xz = __shfl(v.x, v.zl & 63, 64);
-  const float ay_own = v.ra[0] * v.yr[0] + v.ra[1] * v.yr[1];
-  const float ay_z = v.rz[0] * v.yr[0] + v.rz[1] * v.yr[1];
-  const float a1 = __shfl(ay_z, (v.lane + 63) & 63, 64), a2 = __shfl(ay_z, (v.lane + 62) & 63, 64);
-  const float aty = v.valid ? (ay_own + (v.comp == 2 ? (a1 + a2) : 0.0f)) : 0.0f;
-  const float rd = v.valid ? (v.qv + pxh + aty) : 0.0f;
-  float ax[2], rp[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    ax[k] = (k < v.nrow) ? v.ra[k] * v.x + v.rz[k] * xz : 0.0f;
-    rp[k] = (k < v.nrow) ? ax[k] - v.zr[k] : 0.0f;
-  }
-  o[0] = fmaxf(fabsf(v.Einv[0] * rp[0]), fabsf(v.Einv[1] * rp[1]));
-  o[1] = fmaxf(fabsf(v.Einv[0] * v.zr[0]), fabsf(v.Einv[1] * v.zr[1]));
-  o[2] = fmaxf(fabsf(v.Einv[0] * ax[0]), fabsf(v.Einv[1] * ax[1]));
-  o[3] = fabsf(v.Dinv * rd);
-  o[4] = fabsf(v.Dinv * v.qv);
-  o[5] = fabsf(v.Dinv * aty);
-  o[6] = fabsf(v.Dinv * pxh);
-  o[7] = fmaxf(fabsf(rp[0]), fabsf(rp[1]));
-  o[8] = fmaxf(fabsf(v.zr[0]), fabsf(v.zr[1]));
-  o[9] = fmaxf(fabsf(ax[0]), fabsf(ax[1]));
-  o[10] = fabsf(rd);
-  o[11] = fabsf(v.qv);
-  o[12] = fabsf(aty);
-  o[13] = fabsf(pxh);
-  const bool is_sum[14] = {false, false, false, false, false, false, false,
-                           false, false, false, false, false, false, false};
-  block_reduce<W, 14>(o, is_sum, S.red);
+  bsync<W>();
 }
 
 template <int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ? 2 : 1))) void srbd_admm_kernel(const SrbdArgs a) {
-  constexpr int NC = 64 * W;
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ? 4 : 2)))
+void srbd_admm_kernel(const SrbdArgs a) {
+  constexpr int NC = 64 * W, NQ = 16 * W;
   __shared__ __attribute__((aligned(16))) SrbdLds<W> S;
   const int t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
   const int64_t b = blockIdx.x;
   if (b >= a.batch) return;
   const int N = a.N;
-  const float dt = a.dt, m = a.mass;
-  const float dtm = dt / m, dt2m = dt * dt / m;
+  const float Nf = (float)N;
+  const float dt = a.dt;
+  const float dtm = dt / a.mass, dt2m = dt * dt / a.mass;
 
   // ---------------- 1. inputs -> LDS (one instance per block)
-  for (int k = t; k < 13; k += NC) S.x0[k] = a.x0[b * 13 + k];
+  if (t < 13) S.x0[t] = a.x0[b * 13 + t];
+  if (t == 0) {  // static indices: kernel-argument arrays never indexed per lane
+#pragma unroll
+    for (int k = 0; k < 13; ++k) S.q2[k] = a.q2[k];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) S.r2[k] = a.r2[k];
+  }
   {
     const int nct = a.contacts_per_step ? 4 * N : 4;
     for (int k = t; k < 4 * N; k += NC)
       S.ct[k] = a.contacts[b * nct + (a.contacts_per_step ? k : (k & 3))] ? 1 : 0;
   }
-  __syncthreads();
+  bsync<W>();
 
   // ---------------- 2. stance enumeration (integer, bit-exact)
   if (wave == 0) {
-    int base = 0;
-    for (int p0 = 0; p0 < 4 * N; p0 += 64) {
-      const int p = p0 + lane;
-      const bool st = (p < 4 * N) && S.ct[p];
-      const uint64_t msk = __ballot(st);
-      const int idx = base + __popcll(msk & ((1ull << lane) - 1ull));
-      if (st) S.legtab[idx] = p;
-      base += __popcll(msk);
-    }
-    if (lane == 0) S.nlegs = base;
-    for (int j = lane; j <= N; j += 64) {
-      int c = 0;
-      for (int p = 0; p < 4 * j; ++p) c += S.ct[p];
-      S.stepstart[j] = c;
+    const bool s0 = (lane < 4 * N) && S.ct[lane];
+    const bool s1 = (64 + lane < 4 * N) && S.ct[64 + lane];
+    const uint64_t m0 = __ballot(s0), m1 = __ballot(s1);
+    const uint64_t below = (1ull << lane) - 1ull;
+    const int c0 = __popcll(m0);
+    if (s0) S.legtab[__popcll(m0 & below)] = lane;
+    if (s1) S.legtab[c0 + __popcll(m1 & below)] = 64 + lane;
+    if (lane == 0) S.nlegs = c0 + __popcll(m1);
+    if (lane <= N) {
+      const int q = 4 * lane;
+      const uint64_t l0 = q >= 64 ? ~0ull : ((1ull << q) - 1ull);
+      const int q1 = q - 64;
+      const uint64_t l1 = q1 <= 0 ? 0ull : ((1ull << q1) - 1ull);
+      S.stepstart[lane] = __popcll(m0 & l0) + __popcll(m1 & l1);
     }
   }
-  __syncthreads();
+  bsync<W>();
   const int nlegs = uni(S.nlegs);
   const int n = 3 * nlegs;
   if (nlegs > kLegsPerWave * W) {  // uniform: host picks W from the batch max
@@ -488,25 +437,21 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ?
     if (t == 0 && a.status) a.status[b] = QLOCO_BAD_SIZE;
     return;
   }
-  LaneVar v;
-  v.t = t;
-  v.lane = lane;
-  {
-    const int lslot = lane / 3;
-    v.comp = lane - 3 * lslot;
-    const int L = kLegsPerWave * wave + lslot;
-    v.valid = (lane < 63) && (L < nlegs);
-    const int pair = v.valid ? S.legtab[L] : 0;
-    v.step = pair >> 2;
-    v.leg = pair & 3;
-    v.zl = (v.comp == 2) ? lane : (lane + 2 - v.comp);
-  }
-  ColMask<W> cm;
+  int ncol[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) {
     int lw = nlegs - kLegsPerWave * w;
     lw = lw < 0 ? 0 : (lw > kLegsPerWave ? kLegsPerWave : lw);
-    cm.wcols[w] = 3 * lw;
+    ncol[w] = 3 * lw;
+  }
+  const int lslot = lane / 3;
+  const int comp = lane - 3 * lslot;
+  const bool valid = (lane < 63) && (kLegsPerWave * wave + lslot < nlegs);
+  int step, leg;
+  {
+    const int pair = valid ? S.legtab[kLegsPerWave * wave + lslot] : 0;
+    step = pair >> 2;
+    leg = pair & 3;
   }
 
   // ---------------- 3. SRBD model terms (ConvexMpc.cpp:111-160, compute_grf :502-549)
@@ -514,8 +459,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ?
   const float cy = cosf(yaw), sy = sinf(yaw);
   // R = [[c,s,0],[-s,c,0],[0,0,1]] (A1RobotControl.cpp:506-508)
   const float R00 = cy, R01 = sy, R10 = -sy, R11 = cy;
-  float Ii[3][3];
+  f4v lo, hi;
   {
+    float Ii[3][3];
     const float *I = a.inertia;
     const float Rm[3][3] = {{R00, R01, 0.f}, {R10, R11, 0.f}, {0.f, 0.f, 1.f}};
     float RI[3][3], Iw[3][3];
@@ -542,48 +488,31 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ?
     Ii[0][2] = (Iw[0][1] * Iw[1][2] - Iw[0][2] * Iw[1][1]) * id;
     Ii[1][2] = (Iw[0][2] * Iw[1][0] - Iw[0][0] * Iw[1][2]) * id;
     Ii[2][2] = (Iw[0][0] * Iw[1][1] - Iw[0][1] * Iw[1][0]) * id;
-  }
-  // this lane's B_d column (rows 6..8) and E = dt A_c B_d column (rows 0..2)
-  {
+    // this lane's B_d column (rows 6..8) and E = dt A_c B_d column (rows 0..2)
     const float *rf = a.feet + b * (a.feet_per_step ? 12 * N : 12) +
-                      (a.feet_per_step ? 12 * v.step : 0) + 3 * v.leg;
+                      (a.feet_per_step ? 12 * step : 0) + 3 * leg;
     const float rx = rf[0], ry = rf[1], rz = rf[2];
-    const int comp = v.comp;
-    float tv0 = comp == 0 ? 0.f : (comp == 1 ? -rz : ry);  // skew(r) e_comp (Utils.cpp:35-41)
-    float tv1 = comp == 0 ? rz : (comp == 1 ? 0.f : -rx);
-    float tv2 = comp == 0 ? -ry : (comp == 1 ? rx : 0.f);
+    const float tv0 = comp == 0 ? 0.f : (comp == 1 ? -rz : ry);  // skew(r) e_comp (Utils.cpp:35-41)
+    const float tv1 = comp == 0 ? rz : (comp == 1 ? 0.f : -rx);
+    const float tv2 = comp == 0 ? -ry : (comp == 1 ? rx : 0.f);
     float ba[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) ba[r] = dt * (Ii[r][0] * tv0 + Ii[r][1] * tv1 + Ii[r][2] * tv2);
-    v.bvr[0] = ba[0];
-    v.bvr[1] = ba[1];
-    v.bvr[2] = ba[2];
-    v.bvr[3] = dt * (R00 * ba[0] + R01 * ba[1]);
-    v.bvr[4] = dt * (R10 * ba[0] + R11 * ba[1]);
-    v.bvr[5] = dt * ba[2];
-    v.bvr[6] = (float)v.step;
-    v.bvr[7] = v.valid ? (float)comp : -1.0f;
-    if (!v.valid) {
-#pragma unroll
-      for (int k = 0; k < 7; ++k) v.bvr[k] = 0.0f;
+    lo = (f4v){ba[0], ba[1], ba[2], dt * (R00 * ba[0] + R01 * ba[1])};
+    hi = (f4v){dt * (R10 * ba[0] + R11 * ba[1]), dt * ba[2], (float)step, (float)comp};
+    if (!valid) {
+      lo = (f4v)(0.0f);
+      hi = (f4v){0.0f, 0.0f, 0.0f, -1.0f};
     }
-    *reinterpret_cast<float4 *>(&S.bv[t][0]) = make_float4(v.bvr[0], v.bvr[1], v.bvr[2], v.bvr[3]);
-    *reinterpret_cast<float4 *>(&S.bv[t][4]) = make_float4(v.bvr[4], v.bvr[5], v.bvr[6], v.bvr[7]);
+    S.bv[t][0] = lo;
+    S.bv[t][1] = hi;
   }
-  v.r2v = v.valid ? a.r2[3 * v.leg + v.comp] : 0.0f;
-  v.bq0 = a.q2[6] * v.bvr[0];
-  v.bq1 = a.q2[7] * v.bvr[1];
-  v.bq2 = a.q2[8] * v.bvr[2];
-  v.eq0 = a.q2[0] * v.bvr[3];
-  v.eq1 = a.q2[1] * v.bvr[4];
-  v.eq2 = a.q2[2] * v.bvr[5];
-  v.linb = v.valid ? a.q2[9 + v.comp] * dtm * dtm : 0.0f;
-  v.line = v.valid ? a.q2[3 + v.comp] * dt2m * dt2m : 0.0f;
+  const float r2v = valid ? S.r2[3 * leg + comp] : 0.0f;
 
   // ---------------- 4. gradient g = Bqp' Q (Aqp x0 - x_ref) (ConvexMpc.cpp:219-221)
   //     free response A_d^{i+1} x0 in closed form (A_c nilpotent)
-  for (int idx = t; idx < 13 * N; idx += NC) {
-    const int i = idx / 13, s = idx - 13 * i;
+  for (int idx = t; idx < 12 * N; idx += NC) {
+    const int i = idx / 12, s = idx - 12 * i;
     const float k = (float)(i + 1);
     const float *x0 = S.x0;
     float xf;
@@ -595,212 +524,286 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ?
       if (s == 5) xf += 0.5f * k * (k - 1.0f) * dt * dt * x0[12];
     } else if (s < 9) {
       xf = x0[s];
-    } else if (s < 12) {
-      xf = x0[s] + (s == 11 ? k * dt * x0[12] : 0.0f);
     } else {
-      xf = x0[12];
+      xf = x0[s] + (s == 11 ? k * dt * x0[12] : 0.0f);
     }
-    S.err[idx] = a.q2[s] * (xf - a.xref[b * 13 * N + idx]);
+    S.err[idx] = S.q2[s] * (xf - a.xref[b * 13 * N + 13 * i + s]);
   }
-  __syncthreads();
-  suffix_sums<W>(S, N);
-  __syncthreads();
-  v.qv = v.valid ? bqp_t_w(S.W0, S.W1, v.step, v.bvr, dtm, dt2m) : 0.0f;
+  bsync<W>();
+  suffix_weights<W>(S, N);
+  bsync<W>();
+  float qv = valid ? bqp_t<W>(S, step, comp, lo, hi, dtm, dt2m) : 0.0f;
 
   // ---------------- 5. P row in registers (unscaled)
   Row<W> K;
-  gen_p_row<W>(S, v, N, cm, K);
+  const PCoef pc = p_coef<W>(S, lo, hi, comp, valid, dtm, dt2m);
+  gen_row<W, false>(S, pc, t, valid, step, comp, Nf, r2v, 1.0f, 0.f, 0.f, 0.f, K);
 
   // ---------------- 6. constraint rows owned by this lane (ConvexMpc.cpp:47-59, :227-249)
   //  x lane: rows 0 [1,0, mu] in [0,inf), 1 [1,0,-mu] in (-inf,0]
   //  y lane: rows 2 [0,1, mu] in [0,inf), 3 [0,1,-mu] in (-inf,0]
-  //  z lane: row 4 [0,0,1] in [fz_min, fz_max]
-  v.nrow = v.valid ? (v.comp == 2 ? 1 : 2) : 0;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const bool rvld = k < v.nrow;
-    v.ra[k] = rvld ? 1.0f : 0.0f;
-    v.rz[k] = (rvld && v.comp < 2) ? (k == 0 ? a.mu : -a.mu) : 0.0f;
-    if (v.comp < 2) {
-      v.rl[k] = k == 0 ? 0.0f : -INFINITY;
-      v.ru[k] = k == 0 ? INFINITY : 0.0f;
-    } else {
-      v.rl[k] = a.fz_min;
-      v.ru[k] = a.fz_max;
-    }
-    v.rE[k] = 1.0f;
-  }
-  v.Dr = 1.0f;
-  v.cs = 1.0f;
+  //  z lane: row 4 [0,0,1] in [fz_min, fz_max]; its slot 1 is an inert
+  //  zero row with bounds [0,0] (stays z = y = 0), as are padding lanes.
+  const bool xy = comp < 2;
+  float ra0 = valid ? 1.0f : 0.0f, ra1 = (valid && xy) ? 1.0f : 0.0f;
+  float rz0 = (valid && xy) ? a.mu : 0.0f, rz1 = (valid && xy) ? -a.mu : 0.0f;
+  const float rl0 = !valid ? 0.0f : (xy ? 0.0f : a.fz_min);
+  const float ru0 = !valid ? 0.0f : (xy ? INFINITY : a.fz_max);
+  const float rl1 = (valid && xy) ? -INFINITY : 0.0f;
+  const float ru1 = 0.0f;
+  float rE0 = 1.0f, rE1 = 1.0f, Dr = 1.0f, cs = 1.0f;
 
   // ---------------- 7. modified Ruiz equilibration (OSQP scaling.c)
-  for (int it = 0; it < a.scaling; ++it) {
+  {
     float cnP = 0.0f;
 #pragma unroll
-    for (int c0 = 0; c0 < NC; c0 += 4) {
-      if (!cm.ok(c0)) continue;
+    for (int c = 0; c < NC; ++c) cnP = fmaxf(cnP, fabsf(KE(K, c)));
+    for (int it = 0; it < a.scaling; ++it) {
+      float cnA = fmaxf(fabsf(ra0), fabsf(ra1));
+      const float zmax = fmaxf(fabsf(rz0), fabsf(rz1));
+      const float zm1 = lane_prev(zmax), zm2 = lane_prev(zm1);
+      if (comp == 2) cnA = fmaxf(cnA, fmaxf(zm1, zm2));
+      const float Dt = valid ? 1.0f / sqrtf(limit_scaling(fmaxf(cnP, cnA))) : 1.0f;
+      const float Et0 = valid ? 1.0f / sqrtf(limit_scaling(fmaxf(fabsf(ra0), fabsf(rz0)))) : 1.0f;
+      const float Et1 = (valid && xy) ? 1.0f / sqrtf(limit_scaling(fmaxf(fabsf(ra1), fabsf(rz1)))) : 1.0f;
+      const int buf = it & 1;
+      reinterpret_cast<float *>(&S.bc[buf][0])[t] = Dt;
+      bsync<W>();
+      float cn2 = 0.0f;
+      const f2v Dt2 = (f2v)(Dt);
 #pragma unroll
-      for (int cc = 0; cc < 4; ++cc) cnP = fmaxf(cnP, fabsf(K.get(c0 + cc)));
-    }
-    float cnA = fmaxf(fabsf(v.ra[0]), fabsf(v.ra[1]));
-    const float zmax_own = fmaxf(fabsf(v.rz[0]), fabsf(v.rz[1]));
-    const float zm1 = __shfl(zmax_own, (lane + 63) & 63, 64);
-    const float zm2 = __shfl(zmax_own, (lane + 62) & 63, 64);
-    if (v.comp == 2) cnA = fmaxf(cnA, fmaxf(zm1, zm2));
-    const float Dt = v.valid ? 1.0f / sqrtf(limit_scaling(fmaxf(cnP, cnA))) : 1.0f;
-    float Et[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      Et[k] = (k < v.nrow) ? 1.0f / sqrtf(limit_scaling(fmaxf(fabsf(v.ra[k]), fabsf(v.rz[k])))) : 1.0f;
-    const int buf = it & 1;
-    S.bc[buf][t] = Dt;
-    __syncthreads();
-    float cn2 = 0.0f;
-#pragma unroll
-    for (int c0 = 0; c0 < NC; c0 += 4) {
-      if (!cm.ok(c0)) continue;
-      const float4 d4 = *reinterpret_cast<const float4 *>(&S.bc[buf][c0]);
-      const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        const int c = c0 + cc;
-        K.set(c, K.get(c) * (Dt * dd[cc]));
-        cn2 = fmaxf(cn2, fabsf(K.get(c)));
+      for (int q = 0; q < NQ; ++q) {
+        if ((q & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+        const f4v d4 = S.bc[buf][q];
+        K.k[2 * q] *= Dt2 * (f2v){d4.x, d4.y};
+        K.k[2 * q + 1] *= Dt2 * (f2v){d4.z, d4.w};
+        cn2 = fmaxf(cn2, fmaxf(fmaxf(fabsf(K.k[2 * q].x), fabsf(K.k[2 * q].y)),
+                               fmaxf(fabsf(K.k[2 * q + 1].x), fabsf(K.k[2 * q + 1].y))));
       }
+      // z lane's D for the mu entries of the x/y lanes' rows
+      const float Dn1 = lane_next(Dt), Dn2 = lane_next(Dn1);
+      const float Dz = comp == 0 ? Dn2 : (comp == 1 ? Dn1 : Dt);
+      ra0 *= Et0 * Dt;
+      ra1 *= Et1 * Dt;
+      rz0 *= Et0 * Dz;
+      rz1 *= Et1 * Dz;
+      rE0 *= Et0;
+      rE1 *= Et1;
+      qv *= Dt;
+      Dr *= Dt;
+      // cost scaling: mean column norm of P (= row norm, P symmetric) vs ||q||_inf
+      const float sumP = bsum<W>(valid ? cn2 : 0.0f, S.red);
+      float qm[1] = {valid ? fabsf(qv) : 0.0f};
+      bmax<W, 1>(qm, S.red);
+      // K holds D P D without the cost scale: true norms carry the running cs
+      const float meanP = cs * sumP / (float)(n > 0 ? n : 1);
+      const float ctm = 1.0f / limit_scaling(fmaxf(meanP, limit_scaling(qm[0])));
+      qv *= ctm;
+      cs *= ctm;
+      cnP = cn2 * cs;
     }
-    const float Dz = S.bc[buf][v.zl + 64 * wave];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      v.ra[k] *= Et[k] * Dt;
-      v.rz[k] *= Et[k] * Dz;
-      v.rE[k] *= Et[k];
-    }
-    v.qv *= Dt;
-    v.Dr *= Dt;
-    // cost scaling: mean column norm of P vs ||q||_inf
-    float rv2[2] = {v.valid ? cn2 : 0.0f, v.valid ? fabsf(v.qv) : 0.0f};
-    const bool is_sum2[2] = {true, false};
-    block_reduce<W, 2>(rv2, is_sum2, S.red);
-    const float meanP = rv2[0] / (float)(n > 0 ? n : 1);
-    const float qn = limit_scaling(rv2[1]);
-    const float ct = 1.0f / limit_scaling(fmaxf(meanP, qn));
-    K.scale(ct);
-    v.qv *= ct;
-    v.cs *= ct;
   }
-  v.cinv = 1.0f / v.cs;
-  v.Dinv = 1.0f / v.Dr;
+  const float cinv = 1.0f / cs;
+  const float lh0 = rl0 * rE0, uh0 = ru0 * rE0;
+  // slot 1: (-inf, 0] on x/y lanes (E scaling keeps 0 and inf), inert [0, 0] elsewhere
+  const float lh1 = (valid && xy) ? -INFINITY : 0.0f, uh1 = 0.0f;
+  (void)rl1;
+  (void)ru1;
+  // OSQP set_rho_vec: every SRBD row is a two-sided or one-sided inequality
+  // (rho) except a z row with fz_max - fz_min < RHO_TOL (equality, 1e3 rho);
+  // no row is loose.  The inert slot-1 rows have a zero A row, so their rho
+  // never matters -- rho vector = (eq0 ? 1e3 rho : rho, rho): no VGPRs.
+  const bool eq0 = valid && !xy && (uh0 - lh0 < 1e-4f);
   float rho = fminf(fmaxf(a.rho, 1e-6f), 1e6f);
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    v.Einv[k] = 1.0f / v.rE[k];
-    v.lh[k] = v.rl[k] * v.rE[k];
-    v.uh[k] = v.ru[k] * v.rE[k];
-    // OSQP set_rho_vec: loose / equality / inequality rows
-    if (v.lh[k] < -1e26f && v.uh[k] > 1e26f) v.ctype[k] = -1;
-    else if (v.uh[k] - v.lh[k] < 1e-4f) v.ctype[k] = 1;
-    else v.ctype[k] = 0;
-    v.rv[k] = v.ctype[k] == -1 ? 1e-6f : (v.ctype[k] == 1 ? 1e3f * rho : rho);
-    if (k >= v.nrow) v.rv[k] = 1.0f;  // unused slot (avoid 0-division)
-  }
-  __syncthreads();
+  float rvi = 1.0f / rho;
+  S.Dc[t] = valid ? Dr : 1.0f;
+  S.aux[0][t] = r2v;
+  S.aux[1][t] = rE0;
+  S.aux[2][t] = rE1;
+  S.pair[t] = 4 * step + leg;
+  // ||D^-1 q||_inf and ||q||_inf (scaled) are constant over the iterations
+  float qn[2] = {fabsf(qv / Dr), fabsf(qv)};
+#define RV0 (eq0 ? 1e3f * rho : rho)
+#define RVI0 (eq0 ? 1e-3f * rvi : rvi)
+  bmax<W, 2>(qn, S.red);
 
-  // ---------------- 8. K = P + sigma I + A' rho A, inverse in registers
-  add_leg_block<W>(v, a.sigma, cm, K);
-  invert<W>(S, t, cm, K);
+  // leg block sigma I + A' diag(rho) A (3x3, leg-local)
+  auto leg_block = [&](float &add0, float &add1, float &add2) {
+    const float rv0 = RV0, rv1 = rho;
+    const float d_own = rv0 * ra0 * ra0 + rv1 * ra1 * ra1;
+    const float d_oz = rv0 * ra0 * rz0 + rv1 * ra1 * rz1;
+    const float d_zz = rv0 * rz0 * rz0 + rv1 * rz1 * rz1;
+    const float oz1 = lane_prev(d_oz), oz2 = lane_prev(oz1);
+    const float zz1 = lane_prev(d_zz), zz2 = lane_prev(zz1);
+    if (comp == 0) {
+      add0 = d_own + a.sigma; add1 = 0.0f; add2 = d_oz;
+    } else if (comp == 1) {
+      add0 = 0.0f; add1 = d_own + a.sigma; add2 = d_oz;
+    } else {
+      add0 = oz2; add1 = oz1; add2 = d_own + zz1 + zz2 + a.sigma;
+    }
+    if (!valid) add0 = add1 = add2 = 0.0f;
+  };
+
+  // ---------------- 8. K = cs P + sigma I + A' rho A, inverse in registers
+  float diag;
+  {
+    float add0, add1, add2;
+    leg_block(add0, add1, add2);
+    int cb = t - comp, tt = t;
+    asm volatile("" : "+v"(cb), "+v"(tt));
+    const f2v cs2 = (f2v)(cs);
+    diag = 1.0f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int off = c - cb;
+      float ad = off == 0 ? add0 : 0.0f;  // add* are 0 on padding lanes
+      ad = off == 1 ? add1 : ad;
+      ad = off == 2 ? add2 : ad;
+      const float v = fmaf(KE(K, c), cs2.x, ad);
+      KE(K, c) = v;
+      diag = (c == tt) ? v : diag;
+    }
+  }
+  invert<W>(S, t, ncol, diag, K);
   int rho_updates = 0;
 
   // ---------------- 9. ADMM iterations (OSQP osqp_solve)
-  v.x = 0.0f;
-  v.zr[0] = v.zr[1] = 0.0f;
-  v.yr[0] = v.yr[1] = 0.0f;
+  float x = 0.0f, z0 = 0.0f, z1 = 0.0f, y0 = 0.0f, y1 = 0.0f;
   if (a.warm_start) {
     const int nu = 12 * N, ncn = 20 * N;
     const float *wx = a.warm + b * (nu + ncn);
     const float *wy = wx + nu;
-    v.x = v.valid ? wx[12 * v.step + 3 * v.leg + v.comp] * v.Dinv : 0.0f;
-    const int rbase = 20 * v.step + 5 * v.leg + (v.comp == 0 ? 0 : (v.comp == 1 ? 2 : 4));
-#pragma unroll
-    for (int k = 0; k < 2; ++k) v.yr[k] = (k < v.nrow) ? wy[rbase + k] * v.Einv[k] * v.cs : 0.0f;
-    const float xz = __shfl(v.x, v.zl & 63, 64);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) v.zr[k] = (k < v.nrow) ? v.ra[k] * v.x + v.rz[k] * xz : 0.0f;
+    x = valid ? wx[12 * step + 3 * leg + comp] / Dr : 0.0f;
+    const int rbase = 20 * step + 5 * leg + 2 * comp;
+    y0 = valid ? wy[rbase] / rE0 * cs : 0.0f;
+    y1 = (valid && xy) ? wy[rbase + 1] / rE1 * cs : 0.0f;
+    const float n1 = lane_next(x), n2 = lane_next(n1);
+    const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x);
+    z0 = ra0 * x + rz0 * xz;
+    z1 = ra1 * x + rz1 * xz;
   }
   const float alpha = a.alpha, sigma = a.sigma;
   const int interval = (a.adaptive_rho && a.rho_interval == 0)
                            ? (a.check_termination ? 4 * a.check_termination : 100)
                            : a.rho_interval;
   int status = QLOCO_MAX_ITER, iter;
-  float px_last = 0.0f;
+  float px = 0.0f;  // scaled (P x)_v of the last residual evaluation
   bool can_check = false;
-  const int l1 = (lane + 63) & 63, l2 = (lane + 62) & 63;
+
+  // residual norms (OSQP update_info), all lanes participate.
+  //  o[0] ||E^-1(Ax-z)||  o[1] ||E^-1 z||  o[2] ||E^-1 A x||  o[3] ||D^-1 rd||
+  //  o[4] ||D^-1 A'y||    o[5] ||D^-1 P x||
+  //  r[0..5] the scaled ||Ax-z||, ||z||, ||Ax||, ||rd||, ||A'y||, ||Px|| (rho estimate)
+  auto residuals = [&](float (&o)[6], float (&r)[6], bool want_r) {
+    const float Dr = S.Dc[t];
+    S.xs[t] = valid ? x * Dr : 0.0f;
+    bsync<W>();
+    const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
+    const float pxo = p_times_x<W>(S, N, valid, (int)bhi.z, comp, blo, bhi, S.aux[0][t], x * Dr,
+                                   dtm, dt2m);
+    const float Dinv = __builtin_amdgcn_rcpf(Dr);
+    const float Einv0 = __builtin_amdgcn_rcpf(S.aux[1][t]);
+    const float Einv1 = __builtin_amdgcn_rcpf(S.aux[2][t]);
+    px = cs * Dr * pxo;
+    const float n1 = lane_next(x), n2 = lane_next(n1);
+    const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x);
+    const float ay_own = ra0 * y0 + ra1 * y1;
+    const float ay_z = rz0 * y0 + rz1 * y1;
+    const float p1 = lane_prev(ay_z), p2 = lane_prev(p1);
+    const float aty = valid ? (ay_own + (comp == 2 ? (p1 + p2) : 0.0f)) : 0.0f;
+    const float rd = valid ? (qv + px + aty) : 0.0f;
+    const float ax0 = ra0 * x + rz0 * xz, ax1 = ra1 * x + rz1 * xz;
+    const float rp0 = ax0 - z0, rp1 = ax1 - z1;
+    o[0] = fmaxf(fabsf(Einv0 * rp0), fabsf(Einv1 * rp1));
+    o[1] = fmaxf(fabsf(Einv0 * z0), fabsf(Einv1 * z1));
+    o[2] = fmaxf(fabsf(Einv0 * ax0), fabsf(Einv1 * ax1));
+    o[3] = fabsf(Dinv * rd);
+    o[4] = fabsf(Dinv * aty);
+    o[5] = fabsf(Dinv * px);
+    bmax<W, 6>(o, S.red);
+    if (want_r) {
+      r[0] = fmaxf(fabsf(rp0), fabsf(rp1));
+      r[1] = fmaxf(fabsf(z0), fabsf(z1));
+      r[2] = fmaxf(fabsf(ax0), fabsf(ax1));
+      r[3] = fabsf(rd);
+      r[4] = fabsf(aty);
+      r[5] = fabsf(px);
+      bmax<W, 6>(r, S.red);
+    }
+  };
 
   for (iter = 1; iter <= a.max_iter; ++iter) {
-    const float xp = v.x;
-    const float zp0 = v.zr[0], zp1 = v.zr[1];
+    // compiler-only barrier: LDS-resident tables (bv, Dc, ...) are re-read
+    // where used instead of being hoisted into loop-live registers
+    asm volatile("" ::: "memory");
+    const float xp = x, zp0 = z0, zp1 = z1;
     // rhs = sigma x_prev - q + A'(rho z_prev - y)   (compute_rhs)
-    const float w0 = v.rv[0] * zp0 - v.yr[0], w1 = v.rv[1] * zp1 - v.yr[1];
-    const float own = v.ra[0] * w0 + v.ra[1] * w1;
-    const float tz = v.rz[0] * w0 + v.rz[1] * w1;
-    const float t1 = __shfl(tz, l1, 64), t2 = __shfl(tz, l2, 64);
-    const float rhs = v.valid ? (sigma * xp - v.qv + own + (v.comp == 2 ? (t1 + t2) : 0.0f)) : 0.0f;
+    const float rv0 = RV0, rvi0 = RVI0;
+    const float w0 = rv0 * zp0 - y0, w1 = rho * zp1 - y1;
+    const float own = ra0 * w0 + ra1 * w1;
+    const float tz = rz0 * w0 + rz1 * w1;
+    const float t1 = lane_prev(tz), t2 = lane_prev(t1);
+    const float rhs = valid ? (sigma * xp - qv + own + (comp == 2 ? (t1 + t2) : 0.0f)) : 0.0f;
     const int buf = iter & 1;
-    S.bc[buf][t] = rhs;
-    __syncthreads();
-    // x_tilde = K^-1 rhs  (register-resident matvec)
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+    reinterpret_cast<float *>(&S.bc[buf][0])[t] = rhs;
+    bsync<W>();
+    // x_tilde = K^-1 rhs  (register-resident packed matvec)
+    f2v acc0 = (f2v)(0.0f), acc1 = (f2v)(0.0f), acc2 = (f2v)(0.0f), acc3 = (f2v)(0.0f);
 #pragma unroll
-    for (int c0 = 0; c0 < NC; c0 += 4) {
-      if (!cm.ok(c0)) continue;
-      const float4 r4 = *reinterpret_cast<const float4 *>(&S.bc[buf][c0]);
-      acc0 = fmaf(K.get(c0 + 0), r4.x, acc0);
-      acc1 = fmaf(K.get(c0 + 1), r4.y, acc1);
-      acc2 = fmaf(K.get(c0 + 2), r4.z, acc2);
-      acc3 = fmaf(K.get(c0 + 3), r4.w, acc3);
+    for (int q = 0; q < NQ; q += 2) {
+      const f4v ra = S.bc[buf][q], rb = S.bc[buf][q + 1];
+      acc0 = __builtin_elementwise_fma(K.k[2 * q], (f2v){ra.x, ra.y}, acc0);
+      acc1 = __builtin_elementwise_fma(K.k[2 * q + 1], (f2v){ra.z, ra.w}, acc1);
+      acc2 = __builtin_elementwise_fma(K.k[2 * q + 2], (f2v){rb.x, rb.y}, acc2);
+      acc3 = __builtin_elementwise_fma(K.k[2 * q + 3], (f2v){rb.z, rb.w}, acc3);
     }
-    const float xt = v.valid ? ((acc0 + acc1) + (acc2 + acc3)) : 0.0f;
-    const float xtz = __shfl(xt, v.zl & 63, 64);
+    const f2v s2 = (acc0 + acc1) + (acc2 + acc3);
+    const float xt = valid ? (s2.x + s2.y) : 0.0f;
+    const float n1 = lane_next(xt), n2 = lane_next(n1);
+    const float xtz = comp == 0 ? n2 : (comp == 1 ? n1 : xt);
     // update_x / update_z / update_y
-    v.x = alpha * xt + (1.0f - alpha) * xp;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (k < v.nrow) {
-        const float zt = v.ra[k] * xt + v.rz[k] * xtz;
-        const float zrel = alpha * zt + (1.0f - alpha) * (k == 0 ? zp0 : zp1);
-        const float vv = zrel + v.yr[k] / v.rv[k];
-        const float zn = fminf(fmaxf(vv, v.lh[k]), v.uh[k]);
-        v.yr[k] += v.rv[k] * (zrel - zn);
-        v.zr[k] = zn;
-      }
+    x = alpha * xt + (1.0f - alpha) * xp;
+    {
+      const float zt0 = ra0 * xt + rz0 * xtz, zt1 = ra1 * xt + rz1 * xtz;
+      const float zr0 = alpha * zt0 + (1.0f - alpha) * zp0;
+      const float zr1 = alpha * zt1 + (1.0f - alpha) * zp1;
+      const float zn0 = fminf(fmaxf(zr0 + y0 * rvi0, lh0), uh0);
+      const float zn1 = fminf(fmaxf(zr1 + y1 * rvi, lh1), uh1);
+      y0 += rv0 * (zr0 - zn0);
+      y1 += rho * (zr1 - zn1);
+      z0 = zn0;
+      z1 = zn1;
     }
     can_check = a.check_termination && (iter % a.check_termination == 0);
     const bool do_rho = a.adaptive_rho && interval && (iter % interval == 0);
     if (can_check || do_rho) {
-      float o[14];
-      residuals<W>(S, a, v, N, dtm, dt2m, o, px_last);
-      const float pri_res = o[0], dua_res = v.cinv * o[3];
+      float o[6], r[6];
+      residuals(o, r, do_rho);
+      const float pri_res = o[0], dua_res = cinv * o[3];
       if (can_check) {
         const float eps_p = a.eps_abs + a.eps_rel * fmaxf(o[1], o[2]);
-        const float eps_d = a.eps_abs + a.eps_rel * v.cinv * fmaxf(fmaxf(o[4], o[5]), o[6]);
+        const float eps_d = a.eps_abs + a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
         if (pri_res < eps_p && dua_res < eps_d) {
           status = QLOCO_OK;
           break;
         }
       }
       if (do_rho) {  // compute_rho_estimate + adapt_rho
-        const float pn = o[7] / (fmaxf(o[8], o[9]) + 1e-30f);
-        const float dn = o[10] / (fmaxf(fmaxf(o[11], o[12]), o[13]) + 1e-30f);
+        const float pn = r[0] / (fmaxf(r[1], r[2]) + 1e-30f);
+        const float dn = r[3] / (fmaxf(fmaxf(qn[1], r[4]), r[5]) + 1e-30f);
         float rho_new = rho * sqrtf(pn / (dn + 1e-30f));
         rho_new = fminf(fmaxf(rho_new, 1e-6f), 1e6f);
         if (rho_new > rho * a.rho_tol || rho_new < rho / a.rho_tol) {
           rho = rho_new;
-#pragma unroll
-          for (int k = 0; k < 2; ++k)
-            if (k < v.nrow) v.rv[k] = v.ctype[k] == 0 ? rho : (v.ctype[k] == 1 ? 1e3f * rho : 1e-6f);
-          gen_p_row<W>(S, v, N, cm, K);
-          scale_p_row<W>(S, v, cm, K);
-          add_leg_block<W>(v, sigma, cm, K);
-          invert<W>(S, t, cm, K);
+          rvi = 1.0f / rho;
+          float add0, add1, add2;
+          leg_block(add0, add1, add2);
+          const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
+          const PCoef pc2 = p_coef<W>(S, blo, bhi, comp, valid, dtm, dt2m);
+          const float dg = gen_row<W, true>(S, pc2, t, valid, (int)bhi.z, comp, Nf, S.aux[0][t],
+                                            cs * S.Dc[t], add0, add1, add2, K);
+          invert<W>(S, t, ncol, dg, K);
           rho_updates++;
         }
       }
@@ -809,37 +812,36 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ?
   bool have_px = (status == QLOCO_OK);
   if (iter > a.max_iter) {
     iter = a.max_iter;
-    float o[14];
-    residuals<W>(S, a, v, N, dtm, dt2m, o, px_last);
+    float o[6], r[6];
+    residuals(o, r, false);
     have_px = true;
-    const float pri_res = o[0], dua_res = v.cinv * o[3];
+    const float pri_res = o[0], dua_res = cinv * o[3];
     const float ep = 10.f * a.eps_abs + 10.f * a.eps_rel * fmaxf(o[1], o[2]);
-    const float ed = 10.f * a.eps_abs + 10.f * a.eps_rel * v.cinv * fmaxf(fmaxf(o[4], o[5]), o[6]);
+    const float ed = 10.f * a.eps_abs + 10.f * a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
     status = (pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE : QLOCO_MAX_ITER;
   }
 
   // ---------------- 10. outputs: unscale, objective, scatter to leg slots
   if (!have_px) {
-    float o[14];
-    residuals<W>(S, a, v, N, dtm, dt2m, o, px_last);
+    float o[6], r[6];
+    residuals(o, r, false);
   }
-  const float xu = v.valid ? v.x * v.Dr : 0.0f;
-  float objp[1] = {v.valid ? v.cinv * (0.5f * v.x * px_last + v.qv * v.x) : 0.0f};
-  {
-    const bool is_sum1[1] = {true};
-    block_reduce<W, 1>(objp, is_sum1, S.red);
-  }
-  const bool bad = !isfinite(objp[0]);
+  const float Dr_o = S.Dc[t];
+  const int pr_o = S.pair[t];
+  const int step_o = pr_o >> 2, leg_o = pr_o & 3;
+  const float xu = valid ? x * Dr_o : 0.0f;
+  const float objp = bsum<W>(valid ? cinv * (0.5f * x * px + qv * x) : 0.0f, S.red);
+  const bool bad = !isfinite(objp);
   if (bad) status = QLOCO_NAN;
   if (a.u) {  // full solution (world frame), swing forces exactly 0
     float *uo = a.u + b * 12 * N;
     for (int k = t; k < 12 * N; k += NC) uo[k] = 0.0f;
     __syncthreads();
-    if (v.valid) uo[12 * v.step + 3 * v.leg + v.comp] = bad ? NAN : xu;
+    if (valid) uo[12 * step_o + 3 * leg_o + comp] = bad ? NAN : xu;
   }
   // u0: step-0 forces; optional body frame R' u (A1RobotControl.cpp:596-599)
   S.xs[t] = xu;
-  __syncthreads();
+  bsync<W>();
   if (t < 12) {
     const int lg = t / 3, cp = t - 3 * lg;
     float f0 = 0.f, f1 = 0.f, f2 = 0.f;
@@ -862,17 +864,18 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ?
     float *wy = wx + nu;
     for (int k = t; k < nu + ncn; k += NC) wx[k] = 0.0f;
     __syncthreads();
-    if (v.valid) {
-      wx[12 * v.step + 3 * v.leg + v.comp] = xu;
-      const int rbase = 20 * v.step + 5 * v.leg + (v.comp == 0 ? 0 : (v.comp == 1 ? 2 : 4));
-      for (int k = 0; k < v.nrow; ++k) wy[rbase + k] = v.cinv * v.rE[k] * v.yr[k];
+    if (valid) {
+      wx[12 * step_o + 3 * leg_o + comp] = xu;
+      const int rbase = 20 * step_o + 5 * leg_o + 2 * comp;
+      wy[rbase] = cinv * S.aux[1][t] * y0;
+      if (xy) wy[rbase + 1] = cinv * S.aux[2][t] * y1;
     }
   }
   if (t == 0) {
     if (a.status) a.status[b] = status;
     if (a.iters) a.iters[b] = iter;
     if (a.rho_updates) a.rho_updates[b] = rho_updates;
-    if (a.obj) a.obj[b] = objp[0];
+    if (a.obj) a.obj[b] = objp;
   }
 }
 
@@ -929,6 +932,7 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   if (batch == 0) return QLOCO_OK;
   if (!x0 || !x_ref || !feet || !contacts || !u0) return QLOCO_ERR_ARG;
   if (spec->warm_start && !warm) return QLOCO_ERR_ARG;
+  if (spec->mass <= 0.0f || spec->dt <= 0.0f) return QLOCO_ERR_ARG;
   SrbdArgs a;
   memset(&a, 0, sizeof(a));
   a.N = spec->horizon;

@@ -131,3 +131,26 @@ class BatchedConvexMpc:
             ptr(out.u), ptr(out.status), ptr(out.iters), ptr(out.rho_updates), ptr(out.obj),
             ptr(warm), int(max_legs), C.c_void_p(stream)), "qloco_srbd_solve")
         return out
+
+    def build(self, x0, x_ref, feet, contacts=None, want=("H", "g", "lb", "ub"), stream=None):
+        """Dense condensed-QP build only (ConvexMpc::calculate_qp_mats,
+        ConvexMpc.cpp:162-264) via qloco_srbd_build.  Returns a dict of
+        device tensors among H (B,12N,12N) [symmetric; stored col-major],
+        g (B,12N), lb/ub (B,20N), Aqp (B,13,13N) [col-major (13N x 13)],
+        Bqp (B,12N,13N) [col-major (13N x 12N)]."""
+        import torch
+        B, N = x0.shape[0], self.spec.horizon
+        dev = x0.device
+        self.spec.feet_per_step = 1 if feet.shape[1] == 12 * N and N > 1 else 0
+        if contacts is not None:
+            self.spec.contacts_per_step = 1 if contacts.shape[1] == 4 * N and N > 1 else 0
+        shapes = {"H": (B, 12 * N, 12 * N), "g": (B, 12 * N), "lb": (B, 20 * N),
+                  "ub": (B, 20 * N), "Aqp": (B, 13, 13 * N), "Bqp": (B, 12 * N, 13 * N)}
+        out = {k: torch.empty(shapes[k], dtype=torch.float32, device=dev) for k in want}
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        check(lib().qloco_srbd_build(
+            C.byref(self.spec), B, ptr(x0), ptr(x_ref), ptr(feet), ptr(contacts),
+            ptr(out.get("H")), ptr(out.get("g")), ptr(out.get("lb")), ptr(out.get("ub")),
+            ptr(out.get("Aqp")), ptr(out.get("Bqp")), C.c_void_p(stream)), "qloco_srbd_build")
+        return out

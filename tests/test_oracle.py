@@ -1,0 +1,336 @@
+"""CPU tests of the oracle (test infrastructure) -- no GPU.
+
+1. An independent numpy restatement of the reference's ConvexMpc build
+   (a1_cpp_open_source/src/ConvexMpc.cpp:111-264 and the MPC branch of
+   A1RobotControl::compute_grf, A1RobotControl.cpp:452-600) agrees with the
+   oracle's C build (oracle/srbd.c) -- two restatements, written
+   differently, of the same reference lines.
+2. The closed-form Hessian the GPU kernel uses (nilpotent A_c:
+   H = K0 <b,b>_Q + K2 <e,e>_Q + R, quadrupedal_loco_amd/csrc/qloco_srbd.hip
+   header) reproduces the literal dense B_qp' Q B_qp + R.
+3. The exact solver (EiQuadProg restatement) agrees with scipy's SLSQP on
+   the same QPs, and the OSQP-algorithm ADMM restatement lands within its
+   eps of the exact optimum.
+4. The committed golden fixtures (tests/golden/, made by
+   tests/golden/make_golden.py) are reproduced exactly -- they pin the
+   oracle against drift.  Parity status: unpinned (no reference test pins
+   OSQP / EiQuadProg outputs).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from cases import force_inputs
+from srbd_ref import Instance
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SEED = 20261015
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _build():
+    O.build()
+
+
+# numpy restatement of the build lives in srbd_ref (shared with the GPU build test)
+from srbd_ref import np_A_c, np_B_c, np_build  # noqa: E402
+
+
+@pytest.mark.parametrize("gait,N", [(0, 10), (1, 20), (2, 10), (3, 16)])
+def test_numpy_restatement_matches_oracle_build(gait, N):
+    x0, xr, ft, ct = O.gen_srbd(SEED, N, 6, gait=gait)
+    sp = O.srbd_spec(N=N)
+    A = O.constraints(sp)
+    for b in range(6):
+        H, g, lb, ub = O.build_instance(sp, x0[b], xr[b], ft[b], ct[b])
+        Hn, gn, lbn, ubn, Cn, _, _ = np_build(x0[b], xr[b], ft[b], ct[b], N)
+        assert np.allclose(H, Hn, rtol=1e-10, atol=1e-14 * np.abs(Hn).max())
+        assert np.allclose(g, gn, rtol=1e-10, atol=1e-12 * np.abs(gn).max())
+        assert np.array_equal(lb, lbn) and np.array_equal(ub, ubn)
+        assert np.array_equal(A, Cn)
+
+
+def test_feet_per_step_build():
+    N = 10
+    x0, xr, ft, ct = O.gen_srbd(SEED, N, 2, gait=0)
+    rng = np.random.default_rng(3)
+    feet = np.tile(ft[0], N) + rng.uniform(-0.02, 0.02, 12 * N)
+    sp = O.srbd_spec(N=N)
+    H, g, _, _ = O.build_instance(sp, x0[0], xr[0], feet, ct[0], feet_per_step=1)
+    Hn, gn, *_ = np_build(x0[0], xr[0], feet, ct[0], N, feet_per_step=True)
+    assert np.allclose(H, Hn, rtol=1e-10, atol=1e-14 * np.abs(Hn).max())
+    assert np.allclose(g, gn, rtol=1e-10, atol=1e-12 * np.abs(gn).max())
+
+
+# ---------------------------------------------------------------- closed form used by the kernel
+def closed_form_H(x0, feet, N, dt=0.0025, mass=12.0, I=O.GO1_INERTIA, q_w=O.Q_W, r_w=O.R_W):
+    """The kernel's algebra: A_c nilpotent (A_c^2 B_c = 0), so
+    A_d^k B_d = B_d + k E with E = dt A_c B_d, rows of B_d (6..11) and E
+    (0..5) disjoint:  H_(j,a),(l,b) = K0 <b_a,b_b>_Q + K2 <e_a,e_b>_Q + R."""
+    yaw = float(x0[2])
+    c, s = np.cos(yaw), np.sin(yaw)
+    R = np.array([[c, s, 0], [-s, c, 0], [0, 0, 1]])
+    A_c = np_A_c(yaw)
+    Bd = np_B_c(mass, I, R, feet) * dt
+    E = dt * A_c @ Bd
+    assert np.abs(A_c @ A_c @ Bd).max() == 0.0
+    q2 = 2.0 * np.asarray(q_w)
+    bb = Bd.T @ np.diag(q2) @ Bd
+    ee = E.T @ np.diag(q2) @ E
+    H = np.zeros((12 * N, 12 * N))
+    for j in range(N):
+        for l in range(N):
+            M = max(j, l)
+            K0 = N - M
+            K2 = sum((i - j) * (i - l) for i in range(M, N))
+            H[12 * j:12 * j + 12, 12 * l:12 * l + 12] = K0 * bb + K2 * ee
+    return H + np.diag(np.tile(2.0 * np.asarray(r_w), N))
+
+
+@pytest.mark.parametrize("N", [1, 10, 16, 20])
+def test_closed_form_hessian_matches_dense(N):
+    x0, xr, ft, ct = O.gen_srbd(SEED + N, N, 3, gait=0)
+    sp = O.srbd_spec(N=N)
+    for b in range(3):
+        H, *_ = O.build_instance(sp, x0[b], xr[b], ft[b], ct[b])
+        Hc = closed_form_H(x0[b], ft[b], N)
+        assert np.allclose(H, Hc, rtol=1e-9, atol=1e-13 * np.abs(H).max())
+
+
+# ---------------------------------------------------------------- solvers
+def _slsqp(inst):
+    from scipy.optimize import minimize
+    i, r = inst.idx, inst.rows
+    H, g = inst.H[np.ix_(i, i)], inst.g[i]
+    A, lb, ub = inst.A[np.ix_(r, i)], inst.lb[r], inst.ub[r]
+    cons = []
+    fin_l, fin_u = lb > -1e20, ub < 1e20
+    cons.append({"type": "ineq", "fun": lambda x: (A @ x - lb)[fin_l], "jac": lambda x: A[fin_l]})
+    cons.append({"type": "ineq", "fun": lambda x: (ub - A @ x)[fin_u], "jac": lambda x: -A[fin_u]})
+    x0 = np.zeros(len(i))
+    res = minimize(lambda x: 0.5 * x @ H @ x + g @ x, x0, jac=lambda x: H @ x + g,
+                   constraints=cons, method="SLSQP", options={"maxiter": 500, "ftol": 1e-14})
+    x = np.zeros(12 * inst.N)
+    x[i] = res.x
+    return x
+
+
+@pytest.mark.parametrize("gait", [0, 2])
+def test_exact_solver_matches_slsqp(gait):
+    N = 10
+    x0, xr, ft, ct = O.gen_srbd(SEED, N, 4, gait=gait)
+    sp = O.srbd_spec(N=N)
+    for b in range(4):
+        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
+        xe, st, _ = inst.exact()
+        assert st == 0
+        xs = _slsqp(inst)
+        fe, fs = inst.obj(xe), inst.obj(xs)
+        assert inst.violation(xe) < 1e-9
+        assert fe <= fs + 1e-7 * max(1.0, abs(fs)), (fe, fs)
+        assert abs(fe - fs) < 1e-5 * max(1.0, abs(fs)), (fe, fs)
+
+
+def test_admm_lands_within_eps_of_exact():
+    N = 10
+    x0, xr, ft, ct = O.gen_srbd(SEED, N, 8, gait=0)
+    sp = O.srbd_spec(N=N)
+    for b in range(8):
+        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
+        xe, _, _ = inst.exact()
+        for kind, (xa, info) in (("full", inst.admm_full()), ("reduced", inst.admm_reduced())):
+            assert info.status == 0 and info.iters <= 4000
+            fe, fa = inst.obj(xe), inst.obj(xa)
+            assert fa >= fe - 1e-3 * max(1.0, abs(fe))   # eps-feasible iterates can dip below
+            assert fa - fe < 0.05 * max(1.0, abs(fe))
+            assert inst.violation(xa) < 0.5
+            # swing legs: fz bounds [0,0] + friction rows force zero -- to eps in the
+            # full 12N-variable ADMM, exactly in the stance-only form the GPU solves
+            sw = np.repeat(ct[b] == 0, 3)
+            assert np.abs(xa[sw]).max() <= (0.05 if kind == "full" else 0.0)
+
+
+def test_swing_elimination_is_exact():
+    """The GPU solves only stance variables; the exact optimum of the full
+    QP equals that of the stance-only QP with swing forces zero."""
+    N = 10
+    x0, xr, ft, ct = O.gen_srbd(SEED, N, 3, gait=2)
+    sp = O.srbd_spec(N=N)
+    for b in range(3):
+        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
+        xe, _, _ = inst.exact()
+        i, r = inst.idx, inst.rows
+        xr_, st, _ = O.exact_solve(inst.H[np.ix_(i, i)], inst.g[i], inst.A[np.ix_(r, i)],
+                                   inst.lb[r], inst.ub[r])
+        assert st == 0
+        assert np.allclose(xe[i], xr_, atol=1e-6)
+        assert np.abs(np.delete(xe, i)).max() < 1e-9
+
+
+# ---------------------------------------------------------------- golden fixtures
+@pytest.mark.parametrize("name,N,count,gait", [("srbd_trot_n10.npz", 10, 16, 0),
+                                               ("srbd_mixed_n10.npz", 10, 8, 2),
+                                               ("srbd_pace_n20.npz", 20, 4, 1)])
+def test_srbd_goldens_reproduce(name, N, count, gait):
+    d = np.load(os.path.join(GOLD, name))
+    x0, xr, ft, ct = O.gen_srbd(SEED, N, count, gait=gait)
+    assert np.array_equal(x0, d["x0"]) and np.array_equal(xr, d["x_ref"])
+    assert np.array_equal(ft, d["feet"]) and np.array_equal(ct, d["contacts"])
+    sp = O.srbd_spec(N=N)
+    for b in range(count):
+        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
+        if b == 0:
+            assert np.allclose(inst.H, d["H0"], rtol=1e-12) and np.allclose(inst.g, d["g0"], rtol=1e-12)
+        xe, _, _ = inst.exact()
+        assert np.allclose(xe, d["u_exact"][b], rtol=1e-9, atol=1e-9)
+        xa, info = inst.admm_full()
+        assert info.iters == d["iters_admm"][b]
+        assert np.allclose(xa, d["u_admm"][b], rtol=1e-9, atol=1e-9)
+        xrd, infr = inst.admm_reduced()
+        assert infr.iters == d["iters_admm_reduced"][b]
+        assert np.allclose(xrd, d["u_admm_reduced"][b], rtol=1e-9, atol=1e-9)
+
+
+def test_test_mpc_kat():
+    """Known-answer case on the reference harness's own inputs
+    (a1_cpp_open_source/src/test/test_mpc.cpp:18-91; it prints, not asserts)."""
+    d = np.load(os.path.join(GOLD, "srbd_test_mpc_kat.npz"))
+    N = 10
+    sp = O.srbd_spec(N=N, mass=15.0, inertia=d["inertia"], q_w=d["q_w"], r_w=d["r_w"])
+    inst = Instance(sp, d["x0"], d["x_ref"], d["feet"], d["contacts"])
+    xe, st, _ = inst.exact()
+    assert st == 0 and np.allclose(xe, d["u_exact"], rtol=1e-9, atol=1e-9)
+    F = xe[:12].reshape(4, 3)
+    # swing legs FR, RR carry nothing; stance legs sit on the friction cone
+    assert np.abs(F[[1, 3]]).max() < 1e-9
+    assert np.all(F[[0, 2], 2] > 0)
+    assert np.all(np.abs(F[[0, 2], :2]).max(axis=1) <= 0.3 * F[[0, 2], 2] + 1e-9)
+    xa, info = inst.admm_full()
+    assert info.iters == d["iters_admm"] and np.allclose(xa, d["u_admm"], rtol=1e-9, atol=1e-9)
+
+
+def test_force_qp_golden_replay():
+    d = np.load(os.path.join(GOLD, "force_qp.npz"))
+    ticks, B = d["grf_opt"].shape[:2]
+    prm = O.ForceParams()
+    O.lib().qo_force_params_default(C.byref(prm))
+    states = []
+    for b in range(B):
+        s = O.DynState()
+        O.lib().qo_dyn_init(C.byref(s))
+        states.append(s)
+    rng = np.random.default_rng(7)
+    for t in range(ticks):
+        inp = force_inputs(rng, B)
+        for k in inp:
+            assert np.array_equal(inp[k], d[k][t]), k
+        for b in range(B):
+            dd = lambda k, b=b: np.ascontiguousarray(inp[k][b], dtype=np.float64)
+            O.lib().qo_force_distribution(C.byref(states[b]), O.P(dd("com_des")), O.P(dd("leg_des")),
+                                          O.P(dd("F_force_des")), int(inp["mode"][b]),
+                                          float(inp["y_coef"][b]), O.P(dd("rfoot_des")),
+                                          O.P(dd("lfoot_des")))
+            fe = np.ascontiguousarray(inp["feet_p"][b].reshape(4, 3))
+            st, it = C.c_int(0), C.c_int(0)
+            ok = O.lib().qo_force_opt(C.byref(states[b]), C.byref(prm), O.P(dd("base_p")),
+                                      O.P(fe[0].copy()), O.P(fe[1].copy()), O.P(fe[2].copy()),
+                                      O.P(fe[3].copy()), O.P(dd("FT_total_des")), int(inp["mode"][b]),
+                                      int(inp["right_support"][b]), float(inp["y_coef"][b]),
+                                      C.byref(st), C.byref(it))
+            assert np.array_equal(np.array(states[b].grf_opt[:]), d["grf_opt"][t][b])
+            assert np.array_equal(np.array(states[b].F_leg_guess[:]), d["F_leg_guess"][t][b])
+            assert ok == d["qp_solution"][t][b] and st.value == d["status"][t][b]
+            assert it.value == d["iters"][t][b]
+    for s in states:
+        O.lib().qo_dyn_free(C.byref(s))
+
+
+def test_force_qp_quirks():
+    """skew_hat comma-operator quirk (dynmics_compute.cpp:379-381) and the
+    swing-leg equality patterns (:317-345) are visible in the goldens."""
+    d = np.load(os.path.join(GOLD, "force_qp.npz"))
+    g = d["grf_opt"].reshape(-1, 4, 3)
+    mode = d["mode"].reshape(-1)
+    rs = d["right_support"].reshape(-1)
+    ok = d["qp_solution"].reshape(-1) == 1
+    pats = {(102, 0): [1, 2], (102, 1): [0, 3], (101, 0): [0, 2], (101, 1): [1, 3]}
+    seen = 0
+    for (m, r), legs in pats.items():
+        sel = (mode == m) & (rs == r) & ok
+        if sel.any():
+            assert np.abs(g[sel][:, legs]).max() < 1e-9, (m, r)
+            seen += 1
+    assert seen >= 3
+
+
+def test_body_mpc_golden_replay():
+    d = np.load(os.path.join(GOLD, "body_mpc.npz"))
+    B = d["com_traj"].shape[1]
+    states = []
+    for b in range(B):
+        s = O.BodyState()
+        O.lib().qo_body_init(C.byref(s))
+        states.append(s)
+    for k, i in enumerate(d["i"]):
+        for b in range(B):
+            ct = np.zeros(14)
+            O.lib().qo_body_theta_mpc(C.byref(states[b]), int(i),
+                                      O.P(d["bodyangle_state"][k][b].copy()),
+                                      O.P(d["zmp_ref"][k][b].copy()), O.P(d["angle_ref"][k][b].copy()),
+                                      O.P(d["rfoot_ref"][k][b].copy()), O.P(d["lfoot_ref"][k][b].copy()),
+                                      O.P(d["comacc_ref"][k][b].copy()), O.P(np.zeros(9)), O.P(ct), None)
+            assert np.array_equal(ct, d["com_traj"][k][b]), (i, b)
+            assert [states[b].bjx1, states[b].bjx2, states[b].t_yu] == list(d["bjx"][k][b])
+    for s in states:
+        O.lib().qo_body_free(C.byref(s))
+
+
+def test_body_schedule_constants():
+    """_tx schedule (PRMPCClass.cpp:175-178): round((tx+0.7)/0.025)*0.025 - 1e-5."""
+    d = np.load(os.path.join(GOLD, "body_schedule.npz"))
+    s = O.BodyState()
+    O.lib().qo_body_init(C.byref(s))
+    tx = np.array(s.tx[:])
+    assert np.array_equal(tx, d["tx"])
+    assert s.nsum_mpc == d["nsum_mpc"] and s.nstepx == d["nstepx"]
+    steps = np.diff(tx + 1e-5)
+    assert np.allclose(steps[1:], 0.7, atol=0.0125 + 1e-9)
+    # Indexfind (PRMPCClass.cpp:716-738): smallest j with t < tx(j), minus 1
+    for t in np.linspace(0.0, tx[-1] - 1e-6, 97):
+        j = O.lib().qo_body_indexfind(C.byref(s), float(t))
+        assert j == int(np.argmax(t < tx)) - 1
+    O.lib().qo_body_free(C.byref(s))
+
+
+def test_eiquadprog_matches_slsqp_random():
+    from scipy.optimize import minimize
+    rng = np.random.default_rng(5)
+    for n, p, m in [(4, 0, 8), (8, 0, 16), (12, 3, 24)]:
+        Mx = rng.standard_normal((n, n))
+        G = Mx @ Mx.T + n * np.eye(n)
+        g0 = rng.standard_normal(n) * 3
+        CE = rng.standard_normal((n, p))
+        ce0 = rng.standard_normal(p) * 0.3
+        CI = rng.standard_normal((n, m))
+        ci0 = rng.standard_normal(m) + 0.5
+        ws = O.lib().qo_eqp_create(n, p, m)
+        x = np.zeros(n)
+        st, it = C.c_int(0), C.c_int(0)
+        f = O.lib().qo_eqp_solve(ws, O.P(G.ravel(order="F").copy()), O.P(g0.copy()),
+                                 O.P(CE.ravel(order="F").copy() if p else np.zeros(1)),
+                                 O.P(ce0.copy() if p else np.zeros(1)),
+                                 O.P(CI.ravel(order="F").copy()), O.P(ci0.copy()), O.P(x),
+                                 C.byref(st), C.byref(it))
+        O.lib().qo_eqp_destroy(ws)
+        if st.value != 0:
+            continue
+        cons = [{"type": "ineq", "fun": lambda z: CI.T @ z + ci0, "jac": lambda z: CI.T}]
+        if p:
+            cons.append({"type": "eq", "fun": lambda z: CE.T @ z + ce0, "jac": lambda z: CE.T})
+        res = minimize(lambda z: 0.5 * z @ G @ z + g0 @ z, np.zeros(n), jac=lambda z: G @ z + g0,
+                       constraints=cons, method="SLSQP", options={"ftol": 1e-14, "maxiter": 500})
+        assert abs(f - res.fun) < 1e-6 * max(1.0, abs(res.fun)), (n, p, m, f, res.fun)
+        assert np.allclose(x, res.x, atol=1e-5)
