@@ -33,6 +33,7 @@
 #include <string.h>
 
 #include "qloco_common.hpp"
+#include "qloco_dpp.inc"
 
 namespace qloco {
 
@@ -60,13 +61,13 @@ struct SrbdArgs {
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-// One register row of K / K^-1 as packed pairs; every index is static after
-// unrolling, so SROA keeps it in VGPRs.
+// One register row of K / K^-1; every index is static after unrolling, so
+// SROA keeps it in VGPRs.
 template <int W>
 struct Row {
-  f2v k[32 * W];
+  float k[64 * W];
 };
-#define KE(K, c) ((K).k[(c) >> 1][(c)&1])
+#define KE(K, c) ((K).k[(c)])
 
 template <int W>
 struct SrbdLds {
@@ -81,6 +82,7 @@ struct SrbdLds {
   float r2[12];
   float x0[16];
   float aux[3][NC];         // per var, read off the hot path: 2 r (R diag), E row0, E row1
+  f4v zb[NC];               // per var: scaled bounds (l0, u0, l1, u1) of its 2 slots
   int pair[NC];             // per var: 4*step + leg
   float piv[2];
   float red[W][16];
@@ -285,24 +287,20 @@ __device__ __forceinline__ PCoef p_coef(const SrbdLds<W> &S, f4v lo, f4v hi, int
   return c;
 }
 
-// Row of K = rs * D_c * P_rc + [leg block] (SCALED), or the unscaled P row
-// (!SCALED: rs = 1, D = 1, no leg block).  Padding rows are the identity.
-// Returns the diagonal entry (pivot tracking of invert()).
-template <int W, bool SCALED>
-__device__ __forceinline__ float gen_row(const SrbdLds<W> &S, const PCoef &pc, int t, bool valid,
-                                         int step, int comp, float Nf, float r2v, float rs,
-                                         float add0, float add1, float add2, Row<W> &K) {
+// Unscaled closed-form P row (padding rows: the identity row).
+template <int W>
+__device__ __forceinline__ void gen_p_row(const SrbdLds<W> &S, const PCoef &pc, int t, bool valid,
+                                          int step, int comp, float Nf, float r2v, Row<W> &K) {
   constexpr int NC = 64 * W;
   // opaque copies: keep LICM from hoisting per-column selects out of the ADMM loop
-  int tt = t, cb = t - comp, cp = comp;
+  int tt = t, cp = comp;
   float stf = (float)step;
-  asm volatile("" : "+v"(tt), "+v"(cb), "+v"(cp), "+v"(stf));
-  float diag = 1.0f;
+  // padding lanes have zero coefficients, so only their diagonal needs a 1
+  float dadd = valid ? r2v : 1.0f;
+  asm volatile("" : "+v"(tt), "+v"(cp), "+v"(stf), "+v"(dadd));
 #pragma unroll
   for (int c4 = 0; c4 < NC; c4 += 4) {
-    f4v d4 = (f4v)(1.0f);
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges: one 4-column group at a time
-    if constexpr (SCALED) d4 = *reinterpret_cast<const f4v *>(&S.Dc[c4]);
 #pragma unroll
     for (int cc = 0; cc < 4; ++cc) {
       const int c = c4 + cc;
@@ -313,74 +311,128 @@ __device__ __forceinline__ float gen_row(const SrbdLds<W> &S, const PCoef &pc, i
       const float beta = pc.bq0 * lo.x + pc.bq1 * lo.y + pc.bq2 * lo.z + (same ? pc.linb : 0.0f);
       const float epsv = pc.eq0 * lo.w + pc.eq1 * hi.x + pc.eq2 * hi.y + (same ? pc.line : 0.0f);
       float pv = K0 * beta + K2 * epsv;
-      pv += (c == tt) ? r2v : 0.0f;
-      if constexpr (SCALED) {
-        const int off = c - cb;
-        float ad = off == 0 ? add0 : 0.0f;
-        ad = off == 1 ? add1 : ad;
-        ad = off == 2 ? add2 : ad;
-        pv = fmaf(pv, rs * d4[cc], ad);
-      }
-      pv = valid ? pv : ((c == tt) ? 1.0f : 0.0f);
-      diag = (c == tt) ? pv : diag;
+      pv += (c == tt) ? dadd : 0.0f;
       KE(K, c) = pv;
     }
+  }
+}
+
+// K_rc <- rs * D_c * P_rc + [sigma I + A' diag(rho) A]_rc, the leg block
+// touching only the lane's own leg columns (static column -> leg map; D_c
+// fanned out from one LDS chunk per lane by DPP).  Returns the diagonal
+// (pivot tracking of the W = 2 inverse).
+template <int W>
+__device__ __forceinline__ float finalize_row(const SrbdLds<W> &S, int t, int cbase, float rs,
+                                              float add0, float add1, float add2, Row<W> &K) {
+  constexpr int NC = 64 * W;
+  const int lane = t & 63;
+  const f4v d0 = reinterpret_cast<const f4v *>(S.Dc)[lane & 15];
+  QL_DPP_MUL64(K.k, 0, d0);
+  if constexpr (W == 2) {
+    const f4v d1 = reinterpret_cast<const f4v *>(S.Dc)[16 + (lane & 15)];
+    QL_DPP_MUL64(K.k, 64, d1);
+  }
+  int cb = cbase, tt = t;
+  asm volatile("" : "+v"(cb), "+v"(tt));
+  float diag = 1.0f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int cl = c & 63, lb = (c & ~63) + 3 * (cl / 3);  // leg base column of c
+    const int o = cl - 3 * (cl / 3);
+    const bool own = (cb == lb);
+    const float ad = own ? (o == 0 ? add0 : (o == 1 ? add1 : add2)) : 0.0f;
+    const float v = fmaf(KE(K, c), rs, ad);
+    KE(K, c) = v;
+    if constexpr (W == 2) diag = (c == tt) ? v : diag;
   }
   return diag;
 }
 
 // In-place Gauss-Jordan inverse of the register-resident SPD K (no
-// pivoting; Ruiz-scaled, so pivots are O(1)).  Row k is broadcast through
-// LDS with entry k replaced by p+1 (p = pivot, tracked per lane in `diag`
-// with the same fma the row update performs).  With g = A_rk / p
-// (g = 1 - 1/p on the pivot lane) ONE shared update
+// pivoting; Ruiz-scaled, so pivots are O(1)).  The pivot row k is broadcast
+// with entry k replaced by p+1.  With g = A_rk / p (g = 1 - 1/p on the
+// pivot lane) ONE shared update
 //   A_rc <- A_rc - g * bcast_c
 // performs the whole GJ step, column k included (non-pivot:
-// A_rk - g(p+1) = -g; pivot: p - (1-1/p)(p+1) = 1/p).  A_rk is read from the
-// broadcast row: GJ on a symmetric matrix keeps A_rk = +A_kr for
-// unprocessed r and -A_kr for processed r (< k).  Only the n valid pivots
-// run; padding rows/columns are identity and never change.
-template <int W>
-__device__ __forceinline__ void invert(SrbdLds<W> &S, int t, const int (&ncol)[W], float diag,
-                                       Row<W> &K) {
-  constexpr int NQ = 16 * W;
-  float *bcf0 = reinterpret_cast<float *>(&S.bc[0][0]);
-  float *bcf1 = reinterpret_cast<float *>(&S.bc[1][0]);
+// A_rk - g(p+1) = -g; pivot: p - (1-1/p)(p+1) = 1/p).  GJ on a symmetric
+// matrix keeps A_kc = +A_ck for unprocessed c and -A_ck for processed
+// c (< k), so for W = 1 every lane writes its own column-k entry (a static
+// register: the pivot loop is unrolled) and the pivot is a v_readlane --
+// one coalesced ds_write_b32 and one ds_read_b128 per pivot, the row fanned
+// out by DPP.  Only the valid pivots run; padding rows / columns are the
+// identity and never change.
+__device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1> &K) {
+  const int lane = t & 63;
 #pragma unroll
-  for (int w = 0; w < W; ++w) {
+  for (int k = 0; k < 64; ++k) {
+    if (k >= ncol) continue;  // wave-uniform; the loop stays fully unrolled (static register k)
+    const int buf = k & 1;
+    float *bcf = reinterpret_cast<float *>(&S.bc[buf][0]);
+    int tt = t;
+    asm volatile("" : "+v"(tt));  // per-pivot compares stay local (no 64 hoisted masks)
+    const float v = K.k[k];  // A_tk
+    const float p = __builtin_bit_cast(
+        float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
+    float e = (tt < k) ? -v : v;
+    e = (tt == k) ? p + 1.0f : e;
+    bcf[tt] = e;
+    bsync<1>();
+    const f4v r0 = S.bc[buf][lane & 15];
+    const float pinv = __builtin_amdgcn_rcpf(p);
+    const float g = (tt == k) ? (1.0f - pinv) : v * pinv;
+    const float ng = -g;
+    QL_DPP_GJ64(K.k, 0, r0, ng);
+  }
+  bsync<1>();
+}
+
+// Two-wave form: the pivot lane writes its row (its register row is the
+// broadcast; the pivot is tracked per lane in `diag`).
+__device__ __forceinline__ void invert_w2(SrbdLds<2> &S, int t, const int (&ncol)[2], float diag,
+                                          Row<2> &K) {
+  const int lane = t & 63;
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
     for (int kk = 0; kk < ncol[w]; ++kk) {
       const int k = 64 * w + kk;
       const int buf = kk & 1;
-      float *bcf = buf ? bcf1 : bcf0;
+      float *bcf = reinterpret_cast<float *>(&S.bc[buf][0]);
       const bool mine = (t == k);
       if (mine) {
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const f2v a = K.k[2 * q], b2 = K.k[2 * q + 1];
-          S.bc[buf][q] = (f4v){a.x, a.y, b2.x, b2.y};
-        }
+        for (int q = 0; q < 32; ++q)
+          S.bc[buf][q] = (f4v){K.k[4 * q], K.k[4 * q + 1], K.k[4 * q + 2], K.k[4 * q + 3]};
         bcf[k] = diag + 1.0f;
         S.piv[buf] = diag;
       }
-      bsync<W>();
+      __syncthreads();
       const float p = S.piv[buf];
-      const float pinv = __builtin_amdgcn_rcpf(p);
       const float akr = bcf[t];
+      const f4v r0 = S.bc[buf][lane & 15], r1 = S.bc[buf][16 + (lane & 15)];
+      const float pinv = __builtin_amdgcn_rcpf(p);
       const float ak = (t < k) ? -akr : akr;
       const float g = mine ? (1.0f - pinv) : ak * pinv;
-      const f2v ng = (f2v)(-g);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        if ((q & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-        const f4v r4 = S.bc[buf][q];
-        K.k[2 * q] = __builtin_elementwise_fma(ng, (f2v){r4.x, r4.y}, K.k[2 * q]);
-        K.k[2 * q + 1] = __builtin_elementwise_fma(ng, (f2v){r4.z, r4.w}, K.k[2 * q + 1]);
-      }
+      const float ng = -g;
+      QL_DPP_GJ64(K.k, 0, r0, ng);
+      QL_DPP_GJ64(K.k, 64, r1, ng);
       diag = fmaf(-g, akr, diag);
     }
   }
-  bsync<W>();
+  __syncthreads();
 }
+
+// Development-only phase timing (tools/phase_timing.py builds a separate
+// library with -DQLOCO_PHASE_TIMING; the product build never defines it).
+#ifdef QLOCO_PHASE_TIMING
+__device__ unsigned int g_phase[1 << 20];
+#define QL_PHASE(i)                                                           \
+  do {                                                                        \
+    const uint64_t _now = __builtin_readcyclecounter();                       \
+    if (t == 0 && b < (1 << 16)) g_phase[b * 16 + (i)] = (unsigned)(_now - _t0); \
+  } while (0)
+#else
+#define QL_PHASE(i) ((void)0)
+#endif
 
 template <int W>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ? 4 : 2)))
@@ -391,6 +443,9 @@ void srbd_admm_kernel(const SrbdArgs a) {
   const int wave = t >> 6, lane = t & 63;
   const int64_t b = blockIdx.x;
   if (b >= a.batch) return;
+#ifdef QLOCO_PHASE_TIMING
+  const uint64_t _t0 = __builtin_readcyclecounter();
+#endif
   const int N = a.N;
   const float Nf = (float)N;
   const float dt = a.dt;
@@ -454,6 +509,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
     leg = pair & 3;
   }
 
+  QL_PHASE(1);
   // ---------------- 3. SRBD model terms (ConvexMpc.cpp:111-160, compute_grf :502-549)
   const float yaw = S.x0[2];
   const float cy = cosf(yaw), sy = sinf(yaw);
@@ -534,12 +590,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
   bsync<W>();
   float qv = valid ? bqp_t<W>(S, step, comp, lo, hi, dtm, dt2m) : 0.0f;
 
-  // ---------------- 5. P row in registers (unscaled)
-  Row<W> K;
-  const PCoef pc = p_coef<W>(S, lo, hi, comp, valid, dtm, dt2m);
-  gen_row<W, false>(S, pc, t, valid, step, comp, Nf, r2v, 1.0f, 0.f, 0.f, 0.f, K);
-
-  // ---------------- 6. constraint rows owned by this lane (ConvexMpc.cpp:47-59, :227-249)
+  QL_PHASE(2);
+  // ---------------- 5. constraint rows owned by this lane (ConvexMpc.cpp:47-59, :227-249)
   //  x lane: rows 0 [1,0, mu] in [0,inf), 1 [1,0,-mu] in (-inf,0]
   //  y lane: rows 2 [0,1, mu] in [0,inf), 3 [0,1,-mu] in (-inf,0]
   //  z lane: row 4 [0,0,1] in [fz_min, fz_max]; its slot 1 is an inert
@@ -549,90 +601,23 @@ void srbd_admm_kernel(const SrbdArgs a) {
   float rz0 = (valid && xy) ? a.mu : 0.0f, rz1 = (valid && xy) ? -a.mu : 0.0f;
   const float rl0 = !valid ? 0.0f : (xy ? 0.0f : a.fz_min);
   const float ru0 = !valid ? 0.0f : (xy ? INFINITY : a.fz_max);
-  const float rl1 = (valid && xy) ? -INFINITY : 0.0f;
-  const float ru1 = 0.0f;
   float rE0 = 1.0f, rE1 = 1.0f, Dr = 1.0f, cs = 1.0f;
-
-  // ---------------- 7. modified Ruiz equilibration (OSQP scaling.c)
-  {
-    float cnP = 0.0f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) cnP = fmaxf(cnP, fabsf(KE(K, c)));
-    for (int it = 0; it < a.scaling; ++it) {
-      float cnA = fmaxf(fabsf(ra0), fabsf(ra1));
-      const float zmax = fmaxf(fabsf(rz0), fabsf(rz1));
-      const float zm1 = lane_prev(zmax), zm2 = lane_prev(zm1);
-      if (comp == 2) cnA = fmaxf(cnA, fmaxf(zm1, zm2));
-      const float Dt = valid ? 1.0f / sqrtf(limit_scaling(fmaxf(cnP, cnA))) : 1.0f;
-      const float Et0 = valid ? 1.0f / sqrtf(limit_scaling(fmaxf(fabsf(ra0), fabsf(rz0)))) : 1.0f;
-      const float Et1 = (valid && xy) ? 1.0f / sqrtf(limit_scaling(fmaxf(fabsf(ra1), fabsf(rz1)))) : 1.0f;
-      const int buf = it & 1;
-      reinterpret_cast<float *>(&S.bc[buf][0])[t] = Dt;
-      bsync<W>();
-      float cn2 = 0.0f;
-      const f2v Dt2 = (f2v)(Dt);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        if ((q & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-        const f4v d4 = S.bc[buf][q];
-        K.k[2 * q] *= Dt2 * (f2v){d4.x, d4.y};
-        K.k[2 * q + 1] *= Dt2 * (f2v){d4.z, d4.w};
-        cn2 = fmaxf(cn2, fmaxf(fmaxf(fabsf(K.k[2 * q].x), fabsf(K.k[2 * q].y)),
-                               fmaxf(fabsf(K.k[2 * q + 1].x), fabsf(K.k[2 * q + 1].y))));
-      }
-      // z lane's D for the mu entries of the x/y lanes' rows
-      const float Dn1 = lane_next(Dt), Dn2 = lane_next(Dn1);
-      const float Dz = comp == 0 ? Dn2 : (comp == 1 ? Dn1 : Dt);
-      ra0 *= Et0 * Dt;
-      ra1 *= Et1 * Dt;
-      rz0 *= Et0 * Dz;
-      rz1 *= Et1 * Dz;
-      rE0 *= Et0;
-      rE1 *= Et1;
-      qv *= Dt;
-      Dr *= Dt;
-      // cost scaling: mean column norm of P (= row norm, P symmetric) vs ||q||_inf
-      const float sumP = bsum<W>(valid ? cn2 : 0.0f, S.red);
-      float qm[1] = {valid ? fabsf(qv) : 0.0f};
-      bmax<W, 1>(qm, S.red);
-      // K holds D P D without the cost scale: true norms carry the running cs
-      const float meanP = cs * sumP / (float)(n > 0 ? n : 1);
-      const float ctm = 1.0f / limit_scaling(fmaxf(meanP, limit_scaling(qm[0])));
-      qv *= ctm;
-      cs *= ctm;
-      cnP = cn2 * cs;
-    }
-  }
-  const float cinv = 1.0f / cs;
-  const float lh0 = rl0 * rE0, uh0 = ru0 * rE0;
-  // slot 1: (-inf, 0] on x/y lanes (E scaling keeps 0 and inf), inert [0, 0] elsewhere
-  const float lh1 = (valid && xy) ? -INFINITY : 0.0f, uh1 = 0.0f;
-  (void)rl1;
-  (void)ru1;
-  // OSQP set_rho_vec: every SRBD row is a two-sided or one-sided inequality
-  // (rho) except a z row with fz_max - fz_min < RHO_TOL (equality, 1e3 rho);
-  // no row is loose.  The inert slot-1 rows have a zero A row, so their rho
-  // never matters -- rho vector = (eq0 ? 1e3 rho : rho, rho): no VGPRs.
-  const bool eq0 = valid && !xy && (uh0 - lh0 < 1e-4f);
-  float rho = fminf(fmaxf(a.rho, 1e-6f), 1e6f);
-  float rvi = 1.0f / rho;
-  S.Dc[t] = valid ? Dr : 1.0f;
   S.aux[0][t] = r2v;
-  S.aux[1][t] = rE0;
-  S.aux[2][t] = rE1;
   S.pair[t] = 4 * step + leg;
-  // ||D^-1 q||_inf and ||q||_inf (scaled) are constant over the iterations
-  float qn[2] = {fabsf(qv / Dr), fabsf(qv)};
+
+  Row<W> K;
+  float cinv = 1.0f, rho = fminf(fmaxf(a.rho, 1e-6f), 1e6f), rvi = 1.0f / rho;
+  bool eq0 = false;
+  float qn[2] = {0.0f, 0.0f};
 #define RV0 (eq0 ? 1e3f * rho : rho)
 #define RVI0 (eq0 ? 1e-3f * rvi : rvi)
-  bmax<W, 2>(qn, S.red);
-
+  f2v ra = (f2v)(0.0f), rz = (f2v)(0.0f);  // packed slot-0/1 A entries (after scaling)
   // leg block sigma I + A' diag(rho) A (3x3, leg-local)
   auto leg_block = [&](float &add0, float &add1, float &add2) {
     const float rv0 = RV0, rv1 = rho;
-    const float d_own = rv0 * ra0 * ra0 + rv1 * ra1 * ra1;
-    const float d_oz = rv0 * ra0 * rz0 + rv1 * ra1 * rz1;
-    const float d_zz = rv0 * rz0 * rz0 + rv1 * rz1 * rz1;
+    const float d_own = rv0 * ra.x * ra.x + rv1 * ra.y * ra.y;
+    const float d_oz = rv0 * ra.x * rz.x + rv1 * ra.y * rz.y;
+    const float d_zz = rv0 * rz.x * rz.x + rv1 * rz.y * rz.y;
     const float oz1 = lane_prev(d_oz), oz2 = lane_prev(oz1);
     const float zz1 = lane_prev(d_zz), zz2 = lane_prev(zz1);
     if (comp == 0) {
@@ -645,87 +630,56 @@ void srbd_admm_kernel(const SrbdArgs a) {
     if (!valid) add0 = add1 = add2 = 0.0f;
   };
 
-  // ---------------- 8. K = cs P + sigma I + A' rho A, inverse in registers
-  float diag;
-  {
-    float add0, add1, add2;
-    leg_block(add0, add1, add2);
-    int cb = t - comp, tt = t;
-    asm volatile("" : "+v"(cb), "+v"(tt));
-    const f2v cs2 = (f2v)(cs);
-    diag = 1.0f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int off = c - cb;
-      float ad = off == 0 ? add0 : 0.0f;  // add* are 0 on padding lanes
-      ad = off == 1 ? add1 : ad;
-      ad = off == 2 ? add2 : ad;
-      const float v = fmaf(KE(K, c), cs2.x, ad);
-      KE(K, c) = v;
-      diag = (c == tt) ? v : diag;
-    }
-  }
-  invert<W>(S, t, ncol, diag, K);
-  int rho_updates = 0;
-
-  // ---------------- 9. ADMM iterations (OSQP osqp_solve)
-  float x = 0.0f, z0 = 0.0f, z1 = 0.0f, y0 = 0.0f, y1 = 0.0f;
-  if (a.warm_start) {
-    const int nu = 12 * N, ncn = 20 * N;
-    const float *wx = a.warm + b * (nu + ncn);
-    const float *wy = wx + nu;
-    x = valid ? wx[12 * step + 3 * leg + comp] / Dr : 0.0f;
-    const int rbase = 20 * step + 5 * leg + 2 * comp;
-    y0 = valid ? wy[rbase] / rE0 * cs : 0.0f;
-    y1 = (valid && xy) ? wy[rbase + 1] / rE1 * cs : 0.0f;
-    const float n1 = lane_next(x), n2 = lane_next(n1);
-    const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x);
-    z0 = ra0 * x + rz0 * xz;
-    z1 = ra1 * x + rz1 * xz;
-  }
-  const float alpha = a.alpha, sigma = a.sigma;
+  // ---------------- 9. ADMM (OSQP osqp_solve) with its (re)factorisations
+  float x = 0.0f;
+  f2v z = (f2v)(0.0f), y = (f2v)(0.0f);
+  f2v rv = (f2v)(0.0f), rvi2 = (f2v)(0.0f);
+  const float alpha = a.alpha, oma = 1.0f - a.alpha, sigma = a.sigma;
+  const int ctm = a.check_termination;
   const int interval = (a.adaptive_rho && a.rho_interval == 0)
-                           ? (a.check_termination ? 4 * a.check_termination : 100)
-                           : a.rho_interval;
-  int status = QLOCO_MAX_ITER, iter;
+                           ? (ctm ? 4 * ctm : 100)
+                           : (a.adaptive_rho ? a.rho_interval : 0);
+  int status = QLOCO_MAX_ITER, iter = 0;
   float px = 0.0f;  // scaled (P x)_v of the last residual evaluation
-  bool can_check = false;
+  bool have_px = false;
+  bool first = true;
+  int rho_updates = 0;
 
   // residual norms (OSQP update_info), all lanes participate.
   //  o[0] ||E^-1(Ax-z)||  o[1] ||E^-1 z||  o[2] ||E^-1 A x||  o[3] ||D^-1 rd||
   //  o[4] ||D^-1 A'y||    o[5] ||D^-1 P x||
   //  r[0..5] the scaled ||Ax-z||, ||z||, ||Ax||, ||rd||, ||A'y||, ||Px|| (rho estimate)
   auto residuals = [&](float (&o)[6], float (&r)[6], bool want_r) {
-    const float Dr = S.Dc[t];
-    S.xs[t] = valid ? x * Dr : 0.0f;
+    const float Drl = S.Dc[t];
+    S.xs[t] = valid ? x * Drl : 0.0f;
     bsync<W>();
     const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
-    const float pxo = p_times_x<W>(S, N, valid, (int)bhi.z, comp, blo, bhi, S.aux[0][t], x * Dr,
+    const float pxo = p_times_x<W>(S, N, valid, (int)bhi.z, comp, blo, bhi, S.aux[0][t], x * Drl,
                                    dtm, dt2m);
-    const float Dinv = __builtin_amdgcn_rcpf(Dr);
-    const float Einv0 = __builtin_amdgcn_rcpf(S.aux[1][t]);
-    const float Einv1 = __builtin_amdgcn_rcpf(S.aux[2][t]);
-    px = cs * Dr * pxo;
+    const float Dinv = __builtin_amdgcn_rcpf(Drl);
+    const f2v Einv = {__builtin_amdgcn_rcpf(S.aux[1][t]), __builtin_amdgcn_rcpf(S.aux[2][t])};
+    px = cs * Drl * pxo;
     const float n1 = lane_next(x), n2 = lane_next(n1);
     const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x);
-    const float ay_own = ra0 * y0 + ra1 * y1;
-    const float ay_z = rz0 * y0 + rz1 * y1;
+    const f2v ay = ra * y, az = rz * y;
+    const float ay_z = az.x + az.y;
     const float p1 = lane_prev(ay_z), p2 = lane_prev(p1);
-    const float aty = valid ? (ay_own + (comp == 2 ? (p1 + p2) : 0.0f)) : 0.0f;
+    const float aty = valid ? ((ay.x + ay.y) + (comp == 2 ? (p1 + p2) : 0.0f)) : 0.0f;
     const float rd = valid ? (qv + px + aty) : 0.0f;
-    const float ax0 = ra0 * x + rz0 * xz, ax1 = ra1 * x + rz1 * xz;
-    const float rp0 = ax0 - z0, rp1 = ax1 - z1;
-    o[0] = fmaxf(fabsf(Einv0 * rp0), fabsf(Einv1 * rp1));
-    o[1] = fmaxf(fabsf(Einv0 * z0), fabsf(Einv1 * z1));
-    o[2] = fmaxf(fabsf(Einv0 * ax0), fabsf(Einv1 * ax1));
+    const f2v ax = ra * x + rz * xz;
+    const f2v rp = ax - z;
+    const f2v erp = Einv * rp, ez = Einv * z, eax = Einv * ax;
+    o[0] = fmaxf(fabsf(erp.x), fabsf(erp.y));
+    o[1] = fmaxf(fabsf(ez.x), fabsf(ez.y));
+    o[2] = fmaxf(fabsf(eax.x), fabsf(eax.y));
     o[3] = fabsf(Dinv * rd);
     o[4] = fabsf(Dinv * aty);
     o[5] = fabsf(Dinv * px);
     bmax<W, 6>(o, S.red);
     if (want_r) {
-      r[0] = fmaxf(fabsf(rp0), fabsf(rp1));
-      r[1] = fmaxf(fabsf(z0), fabsf(z1));
-      r[2] = fmaxf(fabsf(ax0), fabsf(ax1));
+      r[0] = fmaxf(fabsf(rp.x), fabsf(rp.y));
+      r[1] = fmaxf(fabsf(z.x), fabsf(z.y));
+      r[2] = fmaxf(fabsf(ax.x), fabsf(ax.y));
       r[3] = fabsf(rd);
       r[4] = fabsf(aty);
       r[5] = fabsf(px);
@@ -733,85 +687,207 @@ void srbd_admm_kernel(const SrbdArgs a) {
     }
   };
 
-  for (iter = 1; iter <= a.max_iter; ++iter) {
-    // compiler-only barrier: LDS-resident tables (bv, Dc, ...) are re-read
-    // where used instead of being hoisted into loop-live registers
-    asm volatile("" ::: "memory");
-    const float xp = x, zp0 = z0, zp1 = z1;
-    // rhs = sigma x_prev - q + A'(rho z_prev - y)   (compute_rhs)
-    const float rv0 = RV0, rvi0 = RVI0;
-    const float w0 = rv0 * zp0 - y0, w1 = rho * zp1 - y1;
-    const float own = ra0 * w0 + ra1 * w1;
-    const float tz = rz0 * w0 + rz1 * w1;
-    const float t1 = lane_prev(tz), t2 = lane_prev(t1);
-    const float rhs = valid ? (sigma * xp - qv + own + (comp == 2 ? (t1 + t2) : 0.0f)) : 0.0f;
-    const int buf = iter & 1;
-    reinterpret_cast<float *>(&S.bc[buf][0])[t] = rhs;
-    bsync<W>();
-    // x_tilde = K^-1 rhs  (register-resident packed matvec)
-    f2v acc0 = (f2v)(0.0f), acc1 = (f2v)(0.0f), acc2 = (f2v)(0.0f), acc3 = (f2v)(0.0f);
-#pragma unroll
-    for (int q = 0; q < NQ; q += 2) {
-      const f4v ra = S.bc[buf][q], rb = S.bc[buf][q + 1];
-      acc0 = __builtin_elementwise_fma(K.k[2 * q], (f2v){ra.x, ra.y}, acc0);
-      acc1 = __builtin_elementwise_fma(K.k[2 * q + 1], (f2v){ra.z, ra.w}, acc1);
-      acc2 = __builtin_elementwise_fma(K.k[2 * q + 2], (f2v){rb.x, rb.y}, acc2);
-      acc3 = __builtin_elementwise_fma(K.k[2 * q + 3], (f2v){rb.z, rb.w}, acc3);
-    }
-    const f2v s2 = (acc0 + acc1) + (acc2 + acc3);
-    const float xt = valid ? (s2.x + s2.y) : 0.0f;
-    const float n1 = lane_next(xt), n2 = lane_next(n1);
-    const float xtz = comp == 0 ? n2 : (comp == 1 ? n1 : xt);
-    // update_x / update_z / update_y
-    x = alpha * xt + (1.0f - alpha) * xp;
+  // P row (closed form) and Ruiz equilibration, once
+  {
+    const PCoef pc = p_coef<W>(S, lo, hi, comp, valid, dtm, dt2m);
+    gen_p_row<W>(S, pc, t, valid, step, comp, Nf, r2v, K);
+  }
+  {
     {
-      const float zt0 = ra0 * xt + rz0 * xtz, zt1 = ra1 * xt + rz1 * xtz;
-      const float zr0 = alpha * zt0 + (1.0f - alpha) * zp0;
-      const float zr1 = alpha * zt1 + (1.0f - alpha) * zp1;
-      const float zn0 = fminf(fmaxf(zr0 + y0 * rvi0, lh0), uh0);
-      const float zn1 = fminf(fmaxf(zr1 + y1 * rvi, lh1), uh1);
-      y0 += rv0 * (zr0 - zn0);
-      y1 += rho * (zr1 - zn1);
-      z0 = zn0;
-      z1 = zn1;
-    }
-    can_check = a.check_termination && (iter % a.check_termination == 0);
-    const bool do_rho = a.adaptive_rho && interval && (iter % interval == 0);
-    if (can_check || do_rho) {
-      float o[6], r[6];
-      residuals(o, r, do_rho);
-      const float pri_res = o[0], dua_res = cinv * o[3];
-      if (can_check) {
-        const float eps_p = a.eps_abs + a.eps_rel * fmaxf(o[1], o[2]);
-        const float eps_d = a.eps_abs + a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
-        if (pri_res < eps_p && dua_res < eps_d) {
-          status = QLOCO_OK;
-          break;
+      QL_PHASE(3);
+      // ---------------- 7. modified Ruiz equilibration (OSQP scaling.c); K
+      // keeps the unscaled P, row norms of the scaled P = cs D P D come from
+      // the DPP-fanned D chunk
+      float cnP = 0.0f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) cnP = fmaxf(cnP, fabsf(KE(K, c)));
+      for (int it = 0; it < a.scaling; ++it) {
+        float cnA = fmaxf(fabsf(ra0), fabsf(ra1));
+        const float zmax = fmaxf(fabsf(rz0), fabsf(rz1));
+        const float zm1 = lane_prev(zmax), zm2 = lane_prev(zm1);
+        if (comp == 2) cnA = fmaxf(cnA, fmaxf(zm1, zm2));
+        // v_rsq_f32 (1 ulp): the Ruiz factors are heuristics, not exact quantities
+        const float Dt = valid ? __builtin_amdgcn_rsqf(limit_scaling(fmaxf(cnP, cnA))) : 1.0f;
+        const float Et0 = valid ? __builtin_amdgcn_rsqf(limit_scaling(fmaxf(fabsf(ra0), fabsf(rz0)))) : 1.0f;
+        const float Et1 = (valid && xy) ? __builtin_amdgcn_rsqf(limit_scaling(fmaxf(fabsf(ra1), fabsf(rz1)))) : 1.0f;
+        // z lane's D for the mu entries of the x/y lanes' rows
+        const float Dn1 = lane_next(Dt), Dn2 = lane_next(Dn1);
+        const float Dz = comp == 0 ? Dn2 : (comp == 1 ? Dn1 : Dt);
+        ra0 *= Et0 * Dt;
+        ra1 *= Et1 * Dt;
+        rz0 *= Et0 * Dz;
+        rz1 *= Et1 * Dz;
+        rE0 *= Et0;
+        rE1 *= Et1;
+        qv *= Dt;
+        Dr *= Dt;
+        const int buf = it & 1;
+        reinterpret_cast<float *>(&S.bc[buf][0])[t] = Dr;
+        bsync<W>();
+        float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f, t0, t1, t2, t3;
+        {
+          const f4v d0 = S.bc[buf][lane & 15];
+          QL_DPP_ABSMAX64(m0, m1, m2, m3, t0, t1, t2, t3, d0, K.k, 0);
+          if constexpr (W == 2) {
+            const f4v d1 = S.bc[buf][16 + (lane & 15)];
+            QL_DPP_ABSMAX64(m0, m1, m2, m3, t0, t1, t2, t3, d1, K.k, 64);
+          }
         }
+        // row norm of D P D after this pass (without the running cost scale)
+        const float cn2 = Dr * fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+        // cost scaling: mean column norm of P (= row norm, P symmetric) vs ||q||_inf
+        const float sumP = bsum<W>(valid ? cn2 : 0.0f, S.red);
+        float qm[1] = {valid ? fabsf(qv) : 0.0f};
+        bmax<W, 1>(qm, S.red);
+        const float meanP = cs * sumP / (float)(n > 0 ? n : 1);
+        const float ctc = 1.0f / limit_scaling(fmaxf(meanP, limit_scaling(qm[0])));
+        qv *= ctc;
+        cs *= ctc;
+        cnP = cn2 * cs;
       }
-      if (do_rho) {  // compute_rho_estimate + adapt_rho
-        const float pn = r[0] / (fmaxf(r[1], r[2]) + 1e-30f);
-        const float dn = r[3] / (fmaxf(fmaxf(qn[1], r[4]), r[5]) + 1e-30f);
-        float rho_new = rho * sqrtf(pn / (dn + 1e-30f));
-        rho_new = fminf(fmaxf(rho_new, 1e-6f), 1e6f);
-        if (rho_new > rho * a.rho_tol || rho_new < rho / a.rho_tol) {
-          rho = rho_new;
-          rvi = 1.0f / rho;
-          float add0, add1, add2;
-          leg_block(add0, add1, add2);
-          const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
-          const PCoef pc2 = p_coef<W>(S, blo, bhi, comp, valid, dtm, dt2m);
-          const float dg = gen_row<W, true>(S, pc2, t, valid, (int)bhi.z, comp, Nf, S.aux[0][t],
-                                            cs * S.Dc[t], add0, add1, add2, K);
-          invert<W>(S, t, ncol, dg, K);
-          rho_updates++;
-        }
-      }
+      cinv = 1.0f / cs;
+      const float lh0 = rl0 * rE0, uh0 = ru0 * rE0;
+      // slot 1: (-inf, 0] on x/y lanes (E scaling keeps 0 and inf), inert [0, 0] elsewhere
+      const float lh1 = (valid && xy) ? -INFINITY : 0.0f, uh1 = 0.0f;
+      // OSQP set_rho_vec: every SRBD row is a two-sided or one-sided inequality
+      // (rho) except a z row with fz_max - fz_min < RHO_TOL (equality, 1e3 rho);
+      // no row is loose.  The inert slot-1 rows have a zero A row, so their rho
+      // never matters -- rho vector = (eq0 ? 1e3 rho : rho, rho).
+      eq0 = valid && !xy && (uh0 - lh0 < 1e-4f);
+      S.Dc[t] = valid ? Dr : 1.0f;
+      S.aux[1][t] = rE0;
+      S.aux[2][t] = rE1;
+      S.zb[t] = (f4v){lh0, uh0, lh1, uh1};
+      // ||D^-1 q||_inf and ||q||_inf (scaled) are constant over the iterations
+      qn[0] = fabsf(qv / Dr);
+      qn[1] = fabsf(qv);
+      bmax<W, 2>(qn, S.red);
+      ra = (f2v){ra0, ra1};
+      rz = (f2v){rz0, rz1};
+      bsync<W>();
+      QL_PHASE(4);
     }
   }
-  bool have_px = (status == QLOCO_OK);
-  if (iter > a.max_iter) {
-    iter = a.max_iter;
+  // One code path for the first factorisation and every adaptive-rho
+  // refactorisation: K = cs D P D + leg blocks -> K^-1 -> ADMM blocks.
+  for (;;) {
+    // ---------------- 8. K = cs D P D + sigma I + A' rho A, inverse in registers
+    rv = (f2v){RV0, rho};
+    rvi2 = (f2v){RVI0, rvi};
+    {
+      float add0, add1, add2;
+      leg_block(add0, add1, add2);
+      const float dg = finalize_row<W>(S, t, t - comp, cs * S.Dc[t], add0, add1, add2, K);
+      if (first) QL_PHASE(5);
+      if constexpr (W == 1) {
+        (void)dg;
+        invert_w1(S, t, ncol[0], K);
+      } else {
+        invert_w2(S, t, ncol, dg, K);
+      }
+      if (first) QL_PHASE(6);
+    }
+    if (first) {
+      first = false;
+      if (a.warm_start) {
+        const int nu = 12 * N, ncn = 20 * N;
+        const float *wx = a.warm + b * (nu + ncn);
+        const float *wy = wx + nu;
+        x = valid ? wx[12 * step + 3 * leg + comp] / Dr : 0.0f;
+        const int rbase = 20 * step + 5 * leg + 2 * comp;
+        y.x = valid ? wy[rbase] / rE0 * cs : 0.0f;
+        y.y = (valid && xy) ? wy[rbase + 1] / rE1 * cs : 0.0f;
+        const float n1 = lane_next(x), n2 = lane_next(n1);
+        const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x);
+        z = ra * x + rz * xz;
+      }
+    }
+    bool refactor = false;
+
+    // Iterations run in event-free blocks up to the next termination check,
+    // adaptive-rho point or max_iter, so the hot loop carries no modulo tests.
+    while (iter < a.max_iter) {
+      int next = a.max_iter;
+      if (ctm) next = min(next, (iter / ctm + 1) * ctm);
+      if (interval) next = min(next, (iter / interval + 1) * interval);
+      for (; iter < next; ++iter) {
+        // compiler-only barrier: LDS-resident tables (bv, Dc, zb, ...) are
+        // re-read where used instead of being hoisted into loop-live registers
+        asm volatile("" ::: "memory");
+        // rhs = sigma x_prev - q + A'(rho z_prev - y)   (compute_rhs); padding
+        // lanes have zero A rows and q, so their rhs is 0 without a select
+        const f2v w = __builtin_elementwise_fma(rv, z, -y);
+        const f2v aw = ra * w, zw = rz * w;
+        const float tz = zw.x + zw.y;
+        const float t1 = lane_prev(tz), t2 = lane_prev(t1);
+        float rhs = fmaf(sigma, x, (aw.x + aw.y) - qv);
+        rhs += (comp == 2) ? (t1 + t2) : 0.0f;
+        const int buf = iter & 1;
+        reinterpret_cast<float *>(&S.bc[buf][0])[t] = rhs;
+        bsync<W>();
+        // x_tilde = K^-1 rhs: one 16-byte LDS chunk per lane, DPP row_newbcast
+        // fans it out to the register-resident row (qloco_dpp.inc)
+        float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f, acc3 = 0.0f;
+        {
+          const f4v r0 = S.bc[buf][lane & 15];
+          QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r0, K.k, 0);
+          if constexpr (W == 2) {
+            const f4v r1 = S.bc[buf][16 + (lane & 15)];
+            QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r1, K.k, 64);
+          }
+        }
+        const float xt = (acc0 + acc1) + (acc2 + acc3);
+        const float n1 = lane_next(xt), n2 = lane_next(n1);
+        const float xtz = comp == 0 ? n2 : (comp == 1 ? n1 : xt);
+        // update_x / update_z / update_y (relaxation alpha, projection on [l, u])
+        x = fmaf(alpha, xt, oma * x);
+        const f2v zt = __builtin_elementwise_fma(rz, (f2v)(xtz), ra * xt);
+        const f2v zr = __builtin_elementwise_fma((f2v)(alpha), zt, oma * z);
+        const f2v v = __builtin_elementwise_fma(y, rvi2, zr);
+        const f4v bnd = S.zb[t];  // LDS, not a loop-carried register
+        const f2v zn = {__builtin_amdgcn_fmed3f(v.x, bnd.x, bnd.y),
+                        __builtin_amdgcn_fmed3f(v.y, bnd.z, bnd.w)};
+        y = __builtin_elementwise_fma(rv, zr - zn, y);
+        z = zn;
+      }
+      const bool can_check = ctm && (iter % ctm == 0);
+      const bool do_rho = interval && (iter % interval == 0);
+      if (can_check || do_rho) {
+        float o[6], r[6];
+        residuals(o, r, do_rho);
+        have_px = true;
+        const float pri_res = o[0], dua_res = cinv * o[3];
+        if (can_check) {
+          const float eps_p = a.eps_abs + a.eps_rel * fmaxf(o[1], o[2]);
+          const float eps_d = a.eps_abs + a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
+          if (pri_res < eps_p && dua_res < eps_d) {
+            status = QLOCO_OK;
+            break;
+          }
+        }
+        if (do_rho) {  // compute_rho_estimate + adapt_rho
+          const float pn = r[0] / (fmaxf(r[1], r[2]) + 1e-30f);
+          const float dn = r[3] / (fmaxf(fmaxf(qn[1], r[4]), r[5]) + 1e-30f);
+          float rho_new = rho * sqrtf(pn / (dn + 1e-30f));
+          rho_new = fminf(fmaxf(rho_new, 1e-6f), 1e6f);
+          if (rho_new > rho * a.rho_tol || rho_new < rho / a.rho_tol) {
+            rho = rho_new;
+            rvi = 1.0f / rho;
+            rho_updates++;
+            refactor = true;
+            break;
+          }
+        }
+      }
+    }
+    if (!refactor) break;
+    {
+      const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
+      const PCoef pc = p_coef<W>(S, blo, bhi, comp, valid, dtm, dt2m);
+      gen_p_row<W>(S, pc, t, valid, (int)bhi.z, comp, Nf, S.aux[0][t], K);
+    }
+  }
+  if (status != QLOCO_OK) {  // max_iter reached (OSQP: solved inaccurate or max_iter)
     float o[6], r[6];
     residuals(o, r, false);
     have_px = true;
@@ -821,8 +897,9 @@ void srbd_admm_kernel(const SrbdArgs a) {
     status = (pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE : QLOCO_MAX_ITER;
   }
 
+  QL_PHASE(7);
   // ---------------- 10. outputs: unscale, objective, scatter to leg slots
-  if (!have_px) {
+  if (!have_px) {  // max_iter == 0
     float o[6], r[6];
     residuals(o, r, false);
   }
@@ -867,10 +944,11 @@ void srbd_admm_kernel(const SrbdArgs a) {
     if (valid) {
       wx[12 * step_o + 3 * leg_o + comp] = xu;
       const int rbase = 20 * step_o + 5 * leg_o + 2 * comp;
-      wy[rbase] = cinv * S.aux[1][t] * y0;
-      if (xy) wy[rbase + 1] = cinv * S.aux[2][t] * y1;
+      wy[rbase] = cinv * S.aux[1][t] * y.x;
+      if (xy) wy[rbase + 1] = cinv * S.aux[2][t] * y.y;
     }
   }
+  QL_PHASE(8);
   if (t == 0) {
     if (a.status) a.status[b] = status;
     if (a.iters) a.iters[b] = iter;
@@ -918,6 +996,13 @@ extern "C" void qloco_srbd_spec_default(qloco_srbd_spec *s) {
   s->warm_start = 0;
   s->polish = 0;
 }
+
+#ifdef QLOCO_PHASE_TIMING
+extern "C" int qloco_phase_read(unsigned int *host, size_t count) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), count * sizeof(unsigned int), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 
 extern "C" int qloco_srbd_max_stance_vars(void) { return 3 * kLegsPerWave * 2; }
 
