@@ -83,6 +83,8 @@ struct SrbdLds {
   float x0[16];
   float aux[3][NC];         // per var, read off the hot path: 2 r (R diag), E row0, E row1
   f4v zb[NC];               // per var: scaled bounds (l0, u0, l1, u1) of its 2 slots
+  f4v arz[NC];              // per var: scaled A entries (ra0, ra1, rz0, rz1) of its 2 slots
+  float qs[NC];             // per var: scaled q
   int pair[NC];             // per var: 4*step + leg
   float piv[2];
   float red[W][16];
@@ -434,8 +436,13 @@ __device__ unsigned int g_phase[1 << 20];
 #define QL_PHASE(i) ((void)0)
 #endif
 
+#ifndef QLOCO_SRBD_WAVES_PER_EU  // one-wave kernel occupancy: 3 waves/SIMD = 168 VGPRs, ~no spills
+#define QLOCO_SRBD_WAVES_PER_EU 3
+#endif
+
 template <int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 1 ? 4 : 2)))
+__global__ __launch_bounds__(64 * W)
+__attribute__((amdgpu_waves_per_eu(W == 1 ? QLOCO_SRBD_WAVES_PER_EU : 2)))
 void srbd_admm_kernel(const SrbdArgs a) {
   constexpr int NC = 64 * W, NQ = 16 * W;
   __shared__ __attribute__((aligned(16))) SrbdLds<W> S;
@@ -611,9 +618,10 @@ void srbd_admm_kernel(const SrbdArgs a) {
   float qn[2] = {0.0f, 0.0f};
 #define RV0 (eq0 ? 1e3f * rho : rho)
 #define RVI0 (eq0 ? 1e-3f * rvi : rvi)
-  f2v ra = (f2v)(0.0f), rz = (f2v)(0.0f);  // packed slot-0/1 A entries (after scaling)
-  // leg block sigma I + A' diag(rho) A (3x3, leg-local)
+  // leg block sigma I + A' diag(rho) A (3x3, leg-local); scaled A entries from LDS
   auto leg_block = [&](float &add0, float &add1, float &add2) {
+    const f4v arz = S.arz[t];
+    const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
     const float rv0 = RV0, rv1 = rho;
     const float d_own = rv0 * ra.x * ra.x + rv1 * ra.y * ra.y;
     const float d_oz = rv0 * ra.x * rz.x + rv1 * ra.y * rz.y;
@@ -633,7 +641,6 @@ void srbd_admm_kernel(const SrbdArgs a) {
   // ---------------- 9. ADMM (OSQP osqp_solve) with its (re)factorisations
   float x = 0.0f;
   f2v z = (f2v)(0.0f), y = (f2v)(0.0f);
-  f2v rv = (f2v)(0.0f), rvi2 = (f2v)(0.0f);
   const float alpha = a.alpha, oma = 1.0f - a.alpha, sigma = a.sigma;
   const int ctm = a.check_termination;
   const int interval = (a.adaptive_rho && a.rho_interval == 0)
@@ -658,6 +665,9 @@ void srbd_admm_kernel(const SrbdArgs a) {
                                    dtm, dt2m);
     const float Dinv = __builtin_amdgcn_rcpf(Drl);
     const f2v Einv = {__builtin_amdgcn_rcpf(S.aux[1][t]), __builtin_amdgcn_rcpf(S.aux[2][t])};
+    const f4v arz = S.arz[t];
+    const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
+    const float qv = S.qs[t];
     px = cs * Drl * pxo;
     const float n1 = lane_next(x), n2 = lane_next(n1);
     const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x);
@@ -762,8 +772,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
       qn[0] = fabsf(qv / Dr);
       qn[1] = fabsf(qv);
       bmax<W, 2>(qn, S.red);
-      ra = (f2v){ra0, ra1};
-      rz = (f2v){rz0, rz1};
+      S.arz[t] = (f4v){ra0, ra1, rz0, rz1};
+      S.qs[t] = qv;
       bsync<W>();
       QL_PHASE(4);
     }
@@ -772,8 +782,6 @@ void srbd_admm_kernel(const SrbdArgs a) {
   // refactorisation: K = cs D P D + leg blocks -> K^-1 -> ADMM blocks.
   for (;;) {
     // ---------------- 8. K = cs D P D + sigma I + A' rho A, inverse in registers
-    rv = (f2v){RV0, rho};
-    rvi2 = (f2v){RVI0, rvi};
     {
       float add0, add1, add2;
       leg_block(add0, add1, add2);
@@ -799,7 +807,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
         y.y = (valid && xy) ? wy[rbase + 1] / rE1 * cs : 0.0f;
         const float n1 = lane_next(x), n2 = lane_next(n1);
         const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x);
-        z = ra * x + rz * xz;
+        z = (f2v){ra0, ra1} * x + (f2v){rz0, rz1} * xz;
       }
     }
     bool refactor = false;
@@ -810,10 +818,16 @@ void srbd_admm_kernel(const SrbdArgs a) {
       int next = a.max_iter;
       if (ctm) next = min(next, (iter / ctm + 1) * ctm);
       if (interval) next = min(next, (iter / interval + 1) * interval);
+      // block-local copies: dead again in the cold paths below
+      const f4v arz = S.arz[t];
+      const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
+      const float qv = S.qs[t];
+      const f2v rv = {RV0, rho}, rvi2 = {RVI0, rvi};
       for (; iter < next; ++iter) {
         // compiler-only barrier: LDS-resident tables (bv, Dc, zb, ...) are
         // re-read where used instead of being hoisted into loop-live registers
         asm volatile("" ::: "memory");
+        const f4v bnd = S.zb[t];  // projection bounds: LDS, issued early, not loop-carried
         // rhs = sigma x_prev - q + A'(rho z_prev - y)   (compute_rhs); padding
         // lanes have zero A rows and q, so their rhs is 0 without a select
         const f2v w = __builtin_elementwise_fma(rv, z, -y);
@@ -827,13 +841,13 @@ void srbd_admm_kernel(const SrbdArgs a) {
         bsync<W>();
         // x_tilde = K^-1 rhs: one 16-byte LDS chunk per lane, DPP row_newbcast
         // fans it out to the register-resident row (qloco_dpp.inc)
-        float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f, acc3 = 0.0f;
+        float acc0, acc1, acc2, acc3;
         {
           const f4v r0 = S.bc[buf][lane & 15];
           QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r0, K.k, 0);
           if constexpr (W == 2) {
             const f4v r1 = S.bc[buf][16 + (lane & 15)];
-            QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r1, K.k, 64);
+            QL_DPP_MATVEC64_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
           }
         }
         const float xt = (acc0 + acc1) + (acc2 + acc3);
@@ -844,7 +858,6 @@ void srbd_admm_kernel(const SrbdArgs a) {
         const f2v zt = __builtin_elementwise_fma(rz, (f2v)(xtz), ra * xt);
         const f2v zr = __builtin_elementwise_fma((f2v)(alpha), zt, oma * z);
         const f2v v = __builtin_elementwise_fma(y, rvi2, zr);
-        const f4v bnd = S.zb[t];  // LDS, not a loop-carried register
         const f2v zn = {__builtin_amdgcn_fmed3f(v.x, bnd.x, bnd.y),
                         __builtin_amdgcn_fmed3f(v.y, bnd.z, bnd.w)};
         y = __builtin_elementwise_fma(rv, zr - zn, y);
@@ -907,7 +920,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
   const int pr_o = S.pair[t];
   const int step_o = pr_o >> 2, leg_o = pr_o & 3;
   const float xu = valid ? x * Dr_o : 0.0f;
-  const float objp = bsum<W>(valid ? cinv * (0.5f * x * px + qv * x) : 0.0f, S.red);
+  const float objp = bsum<W>(valid ? cinv * (0.5f * x * px + S.qs[t] * x) : 0.0f, S.red);
   const bool bad = !isfinite(objp);
   if (bad) status = QLOCO_NAN;
   if (a.u) {  // full solution (world frame), swing forces exactly 0

@@ -6,7 +6,10 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
-from quadrupedal_loco_amd import srbd
+from quadrupedal_loco_amd import _lib, srbd
+
+if os.environ.get("QLOCO_LIB"):  # experimental variant (tools/variant_lib.py)
+    _lib.LIB_PATH = os.environ["QLOCO_LIB"]
 
 VARIANTS = {
     "default": {},
@@ -34,6 +37,6 @@ for _ in range(reps):
     s.solve(*args, out=out, max_legs=legs)
 e1.record()
 torch.cuda.synchronize()
-print("%-8s B=%6d  %9.1f us/launch  mean iters %.1f  rho_updates %.2f" % (
-    name, B, e0.elapsed_time(e1) / reps * 1e3, out.iters.float().mean().item(),
+print("%-10s %-8s B=%6d  %9.1f us/launch  mean iters %.1f  rho_updates %.2f" % (
+    os.path.basename(os.path.dirname(os.environ.get("QLOCO_LIB", "/prod/x"))), name, B, e0.elapsed_time(e1) / reps * 1e3, out.iters.float().mean().item(),
     out.rho_updates.float().mean().item()), flush=True)
