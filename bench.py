@@ -33,15 +33,31 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 SEED = 20261015
 
 
-def srbd_flops(n, iters, rho_updates, horizon, checks):
-    """Executed useful FP32 flops of one solve of the fused kernel.
-
-    n            stance variables (3 x stance (step, leg) pairs)
-    build        P rows in closed form (~12 flop/entry) + 10 Ruiz passes (2 flop/entry)
-    factorise    Gauss-Jordan inverse, 2 n^3, plus P rebuild/scale (14 n^2), per (1 + rho_updates)
-    iteration    K^-1 matvec 2 n^2 + ~30 n vector/row work
-    check        structured P x and norms, ~70 n, every check_termination (and rho) iteration
+def srbd_flops_alg(horizon, iters, rho_updates):
+    """ALGORITHMIC flops of one solve, SURVEY.md §8(d) (the reference's 12N-variable
+    formulation, whatever this kernel actually executes):
+      F_B   = (N-1) 2*13^3 + N(N-1)/2 * 2*13*13*12     A powers + B_qp blocks
+      F_H   = N(N+1)(N+2)/6 * 2*12*13*12               structure-aware B'QB
+      F_g   = 2*13N*13 + 2*13N*12N                     gradient
+      F_fac = (12N)^3 / 3 per (re)factorisation, R = 1 + rho_updates
+      F_it  = 2(12N)^2 + 4*36N + 10*(12N + 20N)        per ADMM iteration, K = iters
     """
+    N = float(horizon)
+    it = np.asarray(iters, dtype=np.float64)
+    ru = np.asarray(rho_updates, dtype=np.float64)
+    nu = 12.0 * N
+    F_B = (N - 1) * 2 * 13 ** 3 + N * (N - 1) / 2 * 2 * 13 * 13 * 12
+    F_H = N * (N + 1) * (N + 2) / 6 * (2 * 12 * 13 * 12)
+    F_g = 2 * 13 * N * 13 + 2 * 13 * N * nu
+    F_fac = nu ** 3 / 3.0
+    F_it = 2 * nu ** 2 + 4 * 36 * N + 10 * (nu + 20 * N)
+    return F_B + F_H + F_g + it * F_it + (1.0 + ru) * F_fac
+
+
+def srbd_flops_executed(n, iters, rho_updates, horizon, checks):
+    """Useful FP32 flops the fused kernel executes for one solve:
+    stance-only QP (n = 3 x stance (step, leg) pairs), closed-form P rows,
+    Gauss-Jordan inverse (2n^3) per (re)factorisation, K^-1 matvec per iteration."""
     n = np.asarray(n, dtype=np.float64)
     it = np.asarray(iters, dtype=np.float64)
     ru = np.asarray(rho_updates, dtype=np.float64)
@@ -141,9 +157,10 @@ def main():
     rho_up = out.rho_updates.cpu().numpy()
     n_var = 3 * ct.reshape(B, -1).sum(axis=1)
     checks = iters // 25 + iters // 100
-    flops = srbd_flops(n_var, iters, rho_up, N, checks)
-    flops_launch = float(flops.sum())
-    achieved_tflops = flops_launch / (kern_ms.mean() * 1e-3) / 1e12
+    flops_alg = float(srbd_flops_alg(N, iters, rho_up).sum())
+    flops_exec = float(srbd_flops_executed(n_var, iters, rho_up, N, checks).sum())
+    achieved_tflops = flops_alg / (kern_ms.mean() * 1e-3) / 1e12
+    executed_tflops = flops_exec / (kern_ms.mean() * 1e-3) / 1e12
 
     value = B * world * K / elapsed
     res = {
@@ -178,8 +195,14 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4),
             "traffic": None,
-            "note": "FP32 compute-bound (VALU; FP32 vector peak == FP32 MFMA peak 157.3 TF); "
-                    "flops = executed useful flops per launch (%.3g), DESIGN.md §5" % flops_launch,
+            "algorithmic_flops_per_launch": flops_alg,
+            "executed": round(executed_tflops, 3),
+            "executed_frac": round(executed_tflops / PEAK_FP32_TFLOPS, 4),
+            "note": "FP32 compute bound (VALU; FP32 vector peak == FP32 MFMA peak 157.3 TF). "
+                    "achieved = SURVEY.md 8(d) algorithmic flops of the reference's 12N-variable "
+                    "QP (%.3g per launch) / mean kernel time (HIP events on the launch stream); "
+                    "executed = flops this kernel actually performs on the stance-only QP "
+                    "(%.3g per launch), DESIGN.md 5" % (flops_alg, flops_exec),
         },
     }
     tfile = os.path.join(ROOT, "profiles", "traffic_srbd_n%d_b%d.json" % (N, B))

@@ -1,0 +1,210 @@
+/*
+ * qloco.hpp -- C++ host shim with the reference's class / method signatures.
+ *
+ * Drop-in layer for the ROS control loops of jtdingx/quadrupedal_loco: the
+ * classes keep the reference's names, argument meaning and result members,
+ * and run the solves on the MI355X through the C ABI of qloco.h
+ * (libqloco_host.so -> libqloco.so).  Eigen fixed-size matrices of the
+ * reference become column-major `double` arrays of the same shape (Eigen's
+ * default storage: pass `m.data()`); INTEGRATION.md shows the three-line
+ * adapters for the Eigen call sites.
+ *
+ *   QPsolverGpu / QPBaseClassGpu  <- QPsolver / QPsolver_EiQuadProg /
+ *                                    QPBaseClass (rt_mpc_qp/src/QP/QPBaseClass.h:19-73,
+ *                                    QPBaseClass.cpp:20-152)
+ *   Dynamiccclass                 <- go1_rt_control Dynamiccclass
+ *                                    (dynmics_compute.h:59-76; servo.cpp:1224-1228)
+ *   PRMPCClass                    <- rt_mpc_qp PRMPCClass::body_theta_mpc / Indexfind
+ *                                    (PRMPCClass.h:69-71; gait_fast.cpp:620)
+ *   ConvexMpcBatch                <- A1RobotControl::compute_grf MPC branch +
+ *                                    ConvexMpc (A1RobotControl.cpp:452-600)
+ *
+ * Every class is batched over B independent robots (B = 1 is the drop-in
+ * case).  Host arrays are staged to the device on the object's HIP stream;
+ * device-pointer entry points skip the staging.  Failures of the device
+ * path throw qloco::Error (there is no CPU fallback); solver outcomes are
+ * reported like the reference (NaN-free X / qp_solution flags).
+ */
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "qloco.h"
+
+namespace qloco {
+
+class Error : public std::runtime_error {
+ public:
+  Error(const std::string &what, int status);
+  int status;
+};
+
+// Owned device memory + one HIP stream (created on construction).
+class DeviceArena {
+ public:
+  DeviceArena();
+  ~DeviceArena();
+  DeviceArena(const DeviceArena &) = delete;
+  DeviceArena &operator=(const DeviceArena &) = delete;
+  void *alloc(size_t bytes);        // persistent block, freed with the arena
+  void upload(void *dev, const void *host, size_t bytes);
+  void download(void *host, const void *dev, size_t bytes);
+  void sync();
+  void *stream() const { return stream_; }
+
+ private:
+  void *stream_ = nullptr;
+  std::vector<void *> blocks_;
+};
+
+// ------------------------------------------------------------------------
+// QPsolver / QPsolver_EiQuadProg (QPBaseClass.cpp:20-56): min 0.5 x'Gx + g0'x
+// s.t. CE'x + ce0 = 0, CI'x + ci0 >= 0 (EiQuadProg.hpp:15-36), quirk-compatible
+// Goldfarb-Idnani in fp64 on the GPU.  n <= 16, p <= 16, m <= 64.
+class QPsolverGpu {
+ public:
+  explicit QPsolverGpu(int max_batch = 1);
+  ~QPsolverGpu();
+  void resize(const int &nVar, const int &nEq, const int &nIneq);
+  // One QP; matrices column-major (G n*n, CE n*p, CI n*m).  Returns the cost
+  // (+inf when infeasible, as solve_quadprog).  G is left unchanged.
+  double solve(const double *G, const double *g0, const double *CE, const double *ce0,
+               const double *CI, const double *ci0, double *X);
+  // B QPs of the current size; host arrays of B consecutive instances.
+  void solve_batch(int batch, const double *G, const double *g0, const double *CE,
+                   const double *ce0, const double *CI, const double *ci0, double *X,
+                   double *f, int32_t *status);
+  int last_status() const { return last_status_; }
+  int last_iterations() const { return last_iters_; }
+
+ private:
+  int n_ = 0, p_ = 0, m_ = 0, cap_ = 0, max_batch_;
+  DeviceArena arena_;
+  double *dG_ = nullptr, *dg0_ = nullptr, *dCE_ = nullptr, *dce0_ = nullptr, *dCI_ = nullptr,
+         *dci0_ = nullptr, *dX_ = nullptr, *df_ = nullptr;
+  int32_t *dst_ = nullptr, *dit_ = nullptr;
+  int last_status_ = 0, last_iters_ = 0;
+  void ensure(int batch);
+};
+
+// QPBaseClass (QPBaseClass.h:19-73): owns the QP buffers, solveQP() reports
+// success as "no NaN in X" and ignores the cost (QPBaseClass.cpp:126-152).
+class QPBaseClassGpu {
+ public:
+  std::vector<double> G, g0, CE, ce0, CI, ci0, X;
+  int nVars = 0, nEq = 0, nIneq = 0;
+  void resizeQP(const int &nVars, const int &nEq, const int &nIneq);
+  bool solveQP();
+
+ private:
+  QPsolverGpu solver_{1};
+};
+
+// ------------------------------------------------------------------------
+// Dynamiccclass (go1_rt_control/src/whole_body_dynamics/dynmics_compute.h:59-76).
+// force_distribution + force_opt of robot r are staged; the batch runs on
+// the GPU when force_opt is called for the last robot (robot == batch-1),
+// or explicitly with run().  For batch == 1 this is exactly the reference's
+// call sequence (servo.cpp:1224-1228).  Leg order FR, FL, RR, RL.
+class Dynamiccclass {
+ public:
+  explicit Dynamiccclass(int batch = 1, const qloco_force_params *params = nullptr);
+  void force_distribution(const double com_des[3], const double leg_des[12],
+                          const double F_force_des[6], int mode, double y_coefficient,
+                          const double rfoot_des[3], const double lfoot_des[3], int robot = 0);
+  void force_opt(const double base_p[3], const double FR_p[3], const double FL_p[3],
+                 const double RR_p[3], const double RL_p[3], const double FT_total_des[6],
+                 int mode, int right_support, double y_coefficient, int robot = 0);
+  void run();
+  // compute_joint_torques for all legs of all robots (dynmics_compute.cpp:109-138)
+  void compute_joint_torques(const double *Jaco /*B*4*9*/, const int32_t *swing /*B*4*/,
+                             const double *p_des, const double *p_est, const double *pv_des,
+                             const double *pv_est, double *tau /*B*12*/);
+  // reference result members, B consecutive records
+  std::vector<double> grf_opt;      // 12 per robot
+  std::vector<double> F_leg_ref;    // 3x4 col-major per robot
+  std::vector<double> F_leg_guess;  // 12 per robot
+  std::vector<int32_t> qp_solution, status, iters;
+  int batch() const { return batch_; }
+
+ private:
+  int batch_;
+  qloco_force_params prm_;
+  DeviceArena arena_;
+  std::vector<double> h_com_, h_leg_, h_F_, h_rf_, h_lf_, h_base_, h_feet_, h_FT_, h_y_;
+  std::vector<int32_t> h_mode_, h_rs_;
+  double *d_com_, *d_leg_, *d_F_, *d_rf_, *d_lf_, *d_base_, *d_feet_, *d_FT_, *d_y_, *d_Fref_,
+      *d_grf_, *d_guess_;
+  int32_t *d_mode_, *d_rs_, *d_qps_, *d_st_, *d_it_;
+  double *d_jt_ = nullptr;   // joint-torque staging (allocated on first use)
+  int32_t *d_sw_ = nullptr;
+};
+
+// ------------------------------------------------------------------------
+// PRMPCClass::body_theta_mpc (rt_mpc_qp/src/FastMPC/PRMPCClass.h:69-71): the
+// 8-variable body-inclination QP with the reference's member state
+// (thetaxk/thetayk, V_ini, bjx1/bjx2/t_yu), one record per robot.
+class PRMPCClass {
+ public:
+  explicit PRMPCClass(int batch = 1);
+  // Eigen 2x5 / 3x5 inputs as column-major arrays; returns the 14-vector
+  // [thx0, thy0, taux0, tauy0, zmpx0, zmpy0, thx1, thy1, zmpx1, zmpy1, thx2, thy2,
+  //  zmpx2, zmpy2] (PRMPCClass.cpp:696-709).  Nrtfoorpr_gen is unused by the
+  // reference body and accepted for signature compatibility.
+  std::array<double, 14> body_theta_mpc(int i, const double bodyangle_state[4],
+                                        const double zmp_ref[10], const double angle_ref[10],
+                                        const double rfoot_ref[10], const double lfoot_ref[10],
+                                        const double comacc_ref[15],
+                                        const double Nrtfoorpr_gen[9] = nullptr);
+  // B robots at once (host arrays, B consecutive records each); com_traj B*14.
+  void body_theta_mpc_batch(const int32_t *i, const double *bodyangle_state, const double *zmp_ref,
+                            const double *angle_ref, const double *rfoot_ref,
+                            const double *lfoot_ref, const double *comacc_ref, double *com_traj);
+  int Indexfind(double goal_P);
+  std::vector<double> state;  // QLOCO_BODY_STATE_LEN doubles per robot (host mirror)
+
+ private:
+  int batch_;
+  DeviceArena arena_;
+  double *d_state_, *d_in_, *d_traj_, *d_t_;
+  int32_t *d_i_, *d_st_, *d_j_;
+};
+
+// ------------------------------------------------------------------------
+// A1RobotControl::compute_grf, MPC branch (A1RobotControl.cpp:452-600) over B
+// robots: x0 and the desired trajectory are built exactly as :459-497, the
+// batched fused build + OSQP-algorithm ADMM runs on the GPU, and the forces
+// come back in the body frame (root_rot_mat' u, :596-599).  A leg whose
+// solution is NaN keeps its previous output (the reference's isnan guard).
+struct A1MpcState {                // the A1CtrlStates fields compute_grf reads
+  double root_euler[3], root_pos[3], root_ang_vel[3], root_lin_vel[3];
+  double root_rot_mat[9];          // col-major; used for root_lin_vel_d_world
+  double root_euler_d[3], root_pos_d[3], root_ang_vel_d[3], root_lin_vel_d[3];
+  double foot_pos_abs[12];         // 3x4 col-major, legs FL, FR, RL, RR
+  bool contacts[4];
+};
+
+class ConvexMpcBatch {
+ public:
+  ConvexMpcBatch(int batch, const qloco_srbd_spec *spec = nullptr);
+  // foot_forces_grf: B * 12 (3x4 col-major per robot), in/out
+  void compute_grf(const A1MpcState *states, double *foot_forces_grf);
+  // device-resident form (inputs already in HBM): thin wrapper of qloco_srbd_solve_ex
+  void solve_device(const float *x0, const float *x_ref, const float *feet,
+                    const uint8_t *contacts, float *u0, int32_t *status, int32_t *iters);
+  qloco_srbd_spec spec;
+  std::vector<int32_t> status, iters;
+
+ private:
+  int batch_;
+  DeviceArena arena_;
+  float *d_x0_, *d_xr_, *d_feet_, *d_u0_;
+  uint8_t *d_ct_;
+  int32_t *d_st_, *d_it_;
+};
+
+}  // namespace qloco

@@ -80,7 +80,49 @@ def build(verbose=False, jobs=8):
         if verbose:
             print(" ".join(link))
         subprocess.run(link, check=True)
+    build_host(verbose)
     return LIB
+
+
+HOST_SRC = os.path.join(HERE, "host", "qloco_host.cpp")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+# host-only C++ against the HIP runtime (no device code in these TUs)
+HIP_HOST = ["-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include")]
+HIP_LINK = ["-L" + os.path.join(ROCM, "lib"), "-lamdhip64"]
+HOST_LIB = os.path.join(LIBDIR, "libqloco_host.so")
+
+
+def build_host(verbose=False):
+    """C++ shim with the reference's class signatures (include/qloco.hpp) ->
+    libqloco_host.so, linked against libqloco.so (rpath $ORIGIN)."""
+    deps = [HOST_SRC, os.path.join(INCLUDE, "qloco.hpp"), os.path.join(INCLUDE, "qloco.h"), LIB]
+    if not _needs(HOST_LIB, deps):
+        return HOST_LIB
+    cmd = [HIPCC, "-x", "c++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I" + INCLUDE] + HIP_HOST + [
+           HOST_SRC, "-o", HOST_LIB, "-L" + LIBDIR, "-lqloco", "-Wl,-rpath,$ORIGIN"] + HIP_LINK
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return HOST_LIB
+
+
+def build_host_test(oracle_lib, verbose=False):
+    """tests/cpp/test_host (test infrastructure: links the oracle as checker)."""
+    src = os.path.join(ROOT, "tests", "cpp", "test_host.cpp")
+    outdir = os.path.join(ROOT, "tests", "cpp", "_build")
+    os.makedirs(outdir, exist_ok=True)
+    exe = os.path.join(outdir, "test_host")
+    if not _needs(exe, [src, HOST_LIB, LIB, oracle_lib]):
+        return exe
+    cmd = [HIPCC, "-x", "c++", "-O2", "-std=c++17", "-I" + INCLUDE] + HIP_HOST + [
+           "-I" + os.path.join(ROOT, "oracle"), src, "-o", exe, "-L" + LIBDIR, "-lqloco_host",
+           "-lqloco", "-L" + os.path.dirname(oracle_lib), "-lqloco_oracle",
+           "-Wl,-rpath,$ORIGIN/../../../quadrupedal_loco_amd/lib",
+           "-Wl,-rpath,$ORIGIN/../../../oracle/_build"] + HIP_LINK
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return exe
 
 
 if __name__ == "__main__":

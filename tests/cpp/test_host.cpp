@@ -1,0 +1,229 @@
+// test_host.cpp -- GPU test of the C++ host shim (include/qloco.hpp), run by
+// tests/test_host_gpu.py.  Checker: the CPU oracle (oracle/, test
+// infrastructure, linked here only).  Prints "ALL OK" on success.
+//
+//  1. Dynamiccclass on BASELINE config 1 (Go1 stand balance: mode 102,
+//     right_support 2, homing feet, F_sum = (0,0,117.6,0,0,0)) and a
+//     mode/support sweep over 3 ticks: grf_opt vs qo_force_opt within 1e-9.
+//  2. QPsolverGpu / QPBaseClassGpu on random QPs vs qo_eqp_solve.
+//  3. PRMPCClass::body_theta_mpc over a gait window vs qo_body_theta_mpc;
+//     Indexfind bit-exact.
+//  4. ConvexMpcBatch::compute_grf on the inputs of the reference harness
+//     test_mpc.cpp:18-91 (A1, mass 15, contacts FL, RL): forces within 0.5 N
+//     of the exact optimum committed in tests/golden/srbd_test_mpc_kat.npz.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "qloco.hpp"
+
+extern "C" {
+#include "qloco_oracle.h"
+}
+
+static int g_fail = 0;
+#define CHECK(cond, ...)                  \
+  do {                                    \
+    if (!(cond)) {                        \
+      std::printf("FAIL: " __VA_ARGS__);  \
+      std::printf("\n");                  \
+      ++g_fail;                           \
+    }                                     \
+  } while (0)
+
+static bool close(double a, double b, double rtol, double atol) {
+  return std::fabs(a - b) <= atol + rtol * std::fabs(b);
+}
+
+static void test_force_qp() {
+  const double homing[12] = {0.150786, -0.12675, 0.0, 0.150786, 0.12675, 0.0,
+                             -0.225414, -0.12675, 0.0, -0.225414, 0.12675, 0.0};
+  const int B = 8;
+  qloco::Dynamiccclass dyn(B);
+  std::vector<qo_dyn_state> ref(B);
+  qo_force_params prm;
+  qo_force_params_default(&prm);
+  for (auto &s : ref) qo_dyn_init(&s);
+  std::mt19937_64 rng(7);
+  std::uniform_real_distribution<double> U(-0.02, 0.02);
+  const int modes[3] = {102, 101, 103};
+  for (int tick = 0; tick < 3; ++tick) {
+    std::vector<double> base(B * 3), feet(B * 12), F(B * 6), rf(B * 3), lf(B * 3), y(B);
+    std::vector<int> mode(B), rs(B);
+    for (int b = 0; b < B; ++b) {
+      base[b * 3 + 0] = b ? U(rng) : 0.0;
+      base[b * 3 + 1] = b ? U(rng) : 0.0;
+      base[b * 3 + 2] = 0.309458 + (b ? U(rng) : 0.0);
+      for (int k = 0; k < 12; ++k) feet[b * 12 + k] = homing[k] + ((b && k % 3 != 2) ? U(rng) : 0.0);
+      const double m = 12.0, az = b ? 10 * U(rng) : 0.0;
+      F[b * 6 + 0] = b ? 100 * U(rng) : 0.0;
+      F[b * 6 + 1] = b ? 100 * U(rng) : 0.0;
+      F[b * 6 + 2] = m * 9.8 + m * az;
+      F[b * 6 + 3] = F[b * 6 + 4] = F[b * 6 + 5] = 0.0;
+      mode[b] = b ? modes[(b + tick) % 3] : 102;
+      rs[b] = b ? (b + tick) % 3 : 2;  // b = 0: BASELINE config 1 (double support)
+      y[b] = mode[b] == 101 ? 0.75 : (mode[b] == 102 ? 0.0 : 0.11);
+      for (int c = 0; c < 3; ++c) {
+        rf[b * 3 + c] = 0.5 * (feet[b * 12 + c] + feet[b * 12 + 9 + c]);
+        lf[b * 3 + c] = 0.5 * (feet[b * 12 + 3 + c] + feet[b * 12 + 6 + c]);
+      }
+    }
+    for (int b = 0; b < B; ++b) {  // servo.cpp:1224-1228 call sequence
+      dyn.force_distribution(&base[b * 3], &feet[b * 12], &F[b * 6], mode[b], y[b], &rf[b * 3],
+                             &lf[b * 3], b);
+      dyn.force_opt(&base[b * 3], &feet[b * 12], &feet[b * 12 + 3], &feet[b * 12 + 6],
+                    &feet[b * 12 + 9], &F[b * 6], mode[b], rs[b], y[b], b);
+      qo_force_distribution(&ref[b], &base[b * 3], &feet[b * 12], &F[b * 6], mode[b], y[b],
+                            &rf[b * 3], &lf[b * 3]);
+      const int ok = qo_force_opt(&ref[b], &prm, &base[b * 3], &feet[b * 12], &feet[b * 12 + 3],
+                                  &feet[b * 12 + 6], &feet[b * 12 + 9], &F[b * 6], mode[b], rs[b],
+                                  y[b], nullptr, nullptr);
+      CHECK(dyn.qp_solution[b] == ok, "force qp_solution tick %d robot %d", tick, b);
+    }
+    for (int b = 0; b < B; ++b)
+      for (int k = 0; k < 12; ++k) {
+        CHECK(close(dyn.grf_opt[b * 12 + k], ref[b].grf_opt[k], 1e-9, 1e-8),
+              "grf_opt tick %d robot %d [%d] %.12g vs %.12g", tick, b, k, dyn.grf_opt[b * 12 + k],
+              ref[b].grf_opt[k]);
+        CHECK(dyn.F_leg_guess[b * 12 + k] == ref[b].F_leg_guess[k], "F_leg_guess %d %d", b, k);
+      }
+  }
+  // config 1: the four stance legs carry the robot's weight
+  double fz = 0.0;
+  for (int l = 0; l < 4; ++l) fz += dyn.grf_opt[3 * l + 2];
+  CHECK(std::fabs(fz) > 50.0, "stand-balance total fz %.3f", fz);
+  for (auto &s : ref) qo_dyn_free(&s);
+  std::printf("force QP ok (config 1 total fz %.4f N)\n", fz);
+}
+
+static void test_qpsolver() {
+  std::mt19937_64 rng(11);
+  std::normal_distribution<double> N01(0.0, 1.0);
+  const int n = 12, p = 3, m = 24;
+  qloco::QPBaseClassGpu qp;
+  qp.resizeQP(n, p, m);
+  for (int trial = 0; trial < 20; ++trial) {
+    std::vector<double> M(n * n);
+    for (auto &v : M) v = N01(rng);
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c < n; ++c) {
+        double a = 0.0;
+        for (int k = 0; k < n; ++k) a += M[k * n + r] * M[k * n + c];
+        qp.G[c * n + r] = a + (r == c ? n : 0.0);
+      }
+    for (auto &v : qp.g0) v = 3.0 * N01(rng);
+    for (auto &v : qp.CE) v = N01(rng);
+    for (auto &v : qp.ce0) v = 0.3 * N01(rng);
+    for (auto &v : qp.CI) v = N01(rng);
+    for (auto &v : qp.ci0) v = N01(rng) + 0.5;
+    std::vector<double> G = qp.G, x(n);
+    qo_eqp_ws *ws = qo_eqp_create(n, p, m);
+    int st = 0, it = 0;
+    qo_eqp_solve(ws, G.data(), qp.g0.data(), qp.CE.data(), qp.ce0.data(), qp.CI.data(),
+                 qp.ci0.data(), x.data(), &st, &it);
+    qo_eqp_destroy(ws);
+    const bool ok = qp.solveQP();
+    bool ref_ok = true;  // QPBaseClass.cpp:137-150: success = no NaN in X
+    for (double v : x) ref_ok = ref_ok && !std::isnan(v);
+    CHECK(ok == ref_ok, "QPBaseClass success flag trial %d", trial);
+    if (st == QO_OK)
+      for (int k = 0; k < n; ++k)
+        CHECK(close(qp.X[k], x[k], 1e-9, 1e-9), "QP x trial %d [%d] %.12g vs %.12g", trial, k,
+              qp.X[k], x[k]);
+  }
+  std::printf("QPsolver ok\n");
+}
+
+static void test_body_mpc() {
+  qloco::PRMPCClass body(1);
+  qo_body_state ref;
+  qo_body_init(&ref);
+  std::mt19937_64 rng(5);
+  std::normal_distribution<double> N01(0.0, 1.0);
+  for (int i = 96; i < 160; ++i) {
+    double bs[4], zmp[10], ang[10], rf[10], lf[10], acc[15], gen[9] = {0};
+    for (auto &v : bs) v = 0.05 * N01(rng);
+    for (int k = 0; k < 10; ++k) {
+      zmp[k] = 0.02 * N01(rng);
+      ang[k] = 0.02 * N01(rng);
+      rf[k] = 0.05 * N01(rng);
+      lf[k] = 0.05 * N01(rng);
+    }
+    for (auto &v : acc) v = 0.5 * N01(rng);
+    const std::array<double, 14> out = body.body_theta_mpc(i, bs, zmp, ang, rf, lf, acc, gen);
+    double ct[14];
+    int st = 0;
+    qo_body_theta_mpc(&ref, i, bs, zmp, ang, rf, lf, acc, gen, ct, &st);
+    for (int k = 0; k < 14; ++k)
+      CHECK(close(out[k], ct[k], 1e-9, 1e-12), "body i=%d [%d] %.12g vs %.12g", i, k, out[k], ct[k]);
+    if (i >= 100) {
+      CHECK((int)body.state[26] == ref.bjx1 && (int)body.state[27] == ref.bjx2 &&
+                (int)body.state[28] == ref.t_yu,
+            "schedule ints at i=%d", i);
+    }
+  }
+  for (double t = 0.0; t < 17.0; t += 0.37)
+    CHECK(body.Indexfind(t) == qo_body_indexfind(&ref, t), "Indexfind(%.2f)", t);
+  qo_body_free(&ref);
+  std::printf("body MPC ok\n");
+}
+
+static void test_convex_mpc() {
+  qloco_srbd_spec sp;
+  qloco_srbd_spec_default(&sp);
+  sp.mass = 15.0f;  // test_mpc.cpp:19-23
+  const float I[9] = {0.0158533f, 0, 0, 0, 0.0377999f, 0, 0, 0, 0.0456542f};
+  for (int k = 0; k < 9; ++k) sp.inertia[k] = I[k];
+  const float q[13] = {1, 1, 1, 0, 0, 50, 0, 0, 1, 1, 1, 1, 0};  // :52-56
+  for (int k = 0; k < 13; ++k) sp.q_weights[k] = q[k];
+  for (int k = 0; k < 12; ++k) sp.r_weights[k] = 1e-6f;
+  qloco::ConvexMpcBatch mpc(2, &sp);
+  qloco::A1MpcState st[2] = {};
+  for (auto &s : st) {
+    s.root_pos[2] = 0.15;
+    const double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    for (int k = 0; k < 9; ++k) s.root_rot_mat[k] = R[k];
+    const double feet[12] = {0.17, 0.15, -0.35, 0.17, -0.15, -0.35,
+                             -0.17, 0.15, -0.35, -0.17, -0.15, -0.35};
+    for (int k = 0; k < 12; ++k) s.foot_pos_abs[k] = feet[k];
+    s.contacts[0] = true;   // FL
+    s.contacts[1] = false;  // FR
+    s.contacts[2] = true;   // RL
+    s.contacts[3] = false;  // RR
+  }
+  // the harness's x_d sets z from root_pos + v_d,y * t (:83), = root_pos_d[2] at v_d = 0
+  for (auto &s : st) s.root_pos_d[2] = 0.15;
+  double forces[24] = {0};
+  mpc.compute_grf(st, forces);
+  // exact optimum of the same QP (tests/golden/srbd_test_mpc_kat.npz, u_exact[:12])
+  const double ex[12] = {0.0, -12.8370297, 42.790099, 0.0, 0.0, 0.0,
+                         0.0, -12.8370297, 42.790099, 0.0, 0.0, 0.0};
+  for (int b = 0; b < 2; ++b) {
+    CHECK(mpc.status[b] == QLOCO_OK, "compute_grf status %d", mpc.status[b]);
+    for (int k = 0; k < 12; ++k)
+      CHECK(std::fabs(forces[b * 12 + k] - ex[k]) < 0.5, "compute_grf robot %d [%d] %.4f vs %.4f",
+            b, k, forces[b * 12 + k], ex[k]);
+  }
+  std::printf("compute_grf ok: FL (%.3f, %.3f, %.3f) iters %d\n", forces[0], forces[1], forces[2],
+              mpc.iters[0]);
+}
+
+int main() {
+  try {
+    test_force_qp();
+    test_qpsolver();
+    test_body_mpc();
+    test_convex_mpc();
+  } catch (const qloco::Error &e) {
+    std::printf("FAIL: qloco::Error %s (status %d)\n", e.what(), e.status);
+    return 2;
+  }
+  if (g_fail) {
+    std::printf("%d FAILURES\n", g_fail);
+    return 1;
+  }
+  std::printf("ALL OK\n");
+  return 0;
+}

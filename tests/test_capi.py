@@ -132,3 +132,18 @@ def test_argument_validation_without_device_work():
     assert L.qloco_eiquadprog_solve(17, 0, 8, 1, *args) == 4
     assert L.qloco_eiquadprog_solve(8, 0, 65, 1, *args) == 4
     assert L.qloco_eiquadprog_solve(8, 0, 8, 0, *args) == 100  # NULL G even when empty
+
+
+def test_cpp_shim_exports_reference_classes():
+    """libqloco_host.so carries the reference-shaped C++ classes."""
+    import subprocess
+    lib = os.path.join(ROOT, "quadrupedal_loco_amd", "lib", "libqloco_host.so")
+    if not os.path.exists(lib):
+        from quadrupedal_loco_amd import build as qb
+        qb.build()
+    out = subprocess.run(["nm", "-DC", "--defined-only", lib], capture_output=True, text=True).stdout
+    for sym in ("qloco::Dynamiccclass::force_distribution", "qloco::Dynamiccclass::force_opt",
+                "qloco::PRMPCClass::body_theta_mpc", "qloco::PRMPCClass::Indexfind",
+                "qloco::QPsolverGpu::resize", "qloco::QPsolverGpu::solve",
+                "qloco::QPBaseClassGpu::solveQP", "qloco::ConvexMpcBatch::compute_grf"):
+        assert sym in out, sym
