@@ -32,9 +32,11 @@ SOURCES = [
 # The SRBD kernel keeps a 64-wide register row per lane: SLP vectorisation
 # pairs unrelated columns across the unrolled row loops and inflates live
 # ranges into scratch spills, so it is off there (the packed-fp32 matvec and
-# Gauss-Jordan updates are written with explicit float2 ops).
+# Gauss-Jordan updates are written with explicit float2 ops).  Its pivot
+# loops are unrolled in full (static register per pivot column); the two-wave
+# inverse's body exceeds the default pragma-unroll budget, so it is raised.
 EXTRA = {"qloco_gi.hip": ["-ffp-contract=off"], "qloco_force.hip": ["-ffp-contract=off"],
-         "qloco_body.hip": ["-ffp-contract=off"], "qloco_srbd.hip": ["-fno-slp-vectorize"]}
+         "qloco_body.hip": ["-ffp-contract=off"], "qloco_srbd.hip": ["-fno-slp-vectorize", "-mllvm", "-pragma-unroll-threshold=200000"]}
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC]
 

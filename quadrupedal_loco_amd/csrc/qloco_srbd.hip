@@ -87,6 +87,7 @@ struct SrbdLds {
   float qs[NC];             // per var: scaled q
   int pair[NC];             // per var: 4*step + leg
   float piv[2];
+  float colv[W == 1 ? 1 : 2][W == 1 ? 1 : NC];  // W = 2 inverse: pivot column
   float red[W][16];
   int legtab[4 * kMaxN];   // stance pair -> 4*step + leg
   int stepstart[kMaxN + 1];
@@ -388,38 +389,40 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1>
   bsync<1>();
 }
 
-// Two-wave form: the pivot lane writes its row (its register row is the
-// broadcast; the pivot is tracked per lane in `diag`).
-__device__ __forceinline__ void invert_w2(SrbdLds<2> &S, int t, const int (&ncol)[2], float diag,
-                                          Row<2> &K) {
+
+// Two-wave form: the same transposed write, one pivot half per wave (the
+// pivot column register is static inside each half), one s_barrier per
+// pivot, the pivot value through LDS.
+template <int H>
+__device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, Row<2> &K) {
   const int lane = t & 63;
 #pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    for (int kk = 0; kk < ncol[w]; ++kk) {
-      const int k = 64 * w + kk;
-      const int buf = kk & 1;
-      float *bcf = reinterpret_cast<float *>(&S.bc[buf][0]);
-      const bool mine = (t == k);
-      if (mine) {
-#pragma unroll
-        for (int q = 0; q < 32; ++q)
-          S.bc[buf][q] = (f4v){K.k[4 * q], K.k[4 * q + 1], K.k[4 * q + 2], K.k[4 * q + 3]};
-        bcf[k] = diag + 1.0f;
-        S.piv[buf] = diag;
-      }
-      __syncthreads();
-      const float p = S.piv[buf];
-      const float akr = bcf[t];
-      const f4v r0 = S.bc[buf][lane & 15], r1 = S.bc[buf][16 + (lane & 15)];
-      const float pinv = __builtin_amdgcn_rcpf(p);
-      const float ak = (t < k) ? -akr : akr;
-      const float g = mine ? (1.0f - pinv) : ak * pinv;
-      const float ng = -g;
-      QL_DPP_GJ64(K.k, 0, r0, ng);
-      QL_DPP_GJ64(K.k, 64, r1, ng);
-      diag = fmaf(-g, akr, diag);
-    }
+  for (int kk = 0; kk < 64; ++kk) {
+    if (kk >= nw) continue;  // block-uniform
+    const int k = 64 * H + kk;
+    const int buf = kk & 1;
+    float *bcf = reinterpret_cast<float *>(&S.bc[buf][0]);
+    int tt = t;
+    asm volatile("" : "+v"(tt));
+    const float v = K.k[k];  // A_tk
+    float e = (tt < k) ? -v : v;
+    e = (tt == k) ? v + 1.0f : e;
+    bcf[tt] = e;
+    S.colv[buf][tt] = v;  // the pivot A_kk for the other wave (no divergent store)
+    __syncthreads();
+    const float p = S.colv[buf][k];
+    const f4v r0 = S.bc[buf][lane & 15], r1 = S.bc[buf][16 + (lane & 15)];
+    const float pinv = __builtin_amdgcn_rcpf(p);
+    const float g = (tt == k) ? (1.0f - pinv) : v * pinv;
+    const float ng = -g;
+    QL_DPP_GJ64(K.k, 0, r0, ng);
+    QL_DPP_GJ64(K.k, 64, r1, ng);
   }
+}
+
+__device__ __forceinline__ void invert_w2(SrbdLds<2> &S, int t, const int (&ncol)[2], Row<2> &K) {
+  invert_w2_half<0>(S, t, ncol[0], K);
+  invert_w2_half<1>(S, t, ncol[1], K);
   __syncthreads();
 }
 
@@ -791,7 +794,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
         (void)dg;
         invert_w1(S, t, ncol[0], K);
       } else {
-        invert_w2(S, t, ncol, dg, K);
+        (void)dg;
+        invert_w2(S, t, ncol, K);
       }
       if (first) QL_PHASE(6);
     }

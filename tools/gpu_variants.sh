@@ -1,11 +1,13 @@
 #!/bin/bash
-# time the product library and experimental variants: tools/gpu_variants.sh OUT VAR...
+# time experimental builds (tools/_var/NAME/libqloco.so) against the product library
+# usage: bash tools/gpu_variants.sh OUT "VAR1 VAR2 ..." "B1 B2 ..." [N] [GAIT]
 set -o pipefail
-out=$1; shift
+out=$1; vars=$2; bs=$3; n=${4:-10}; gait=${5:-trot}
 mkdir -p $(dirname $out)
-timeout -k 10 300 python -m pytest tests/test_srbd_gpu.py -x -q -m gpu > ${out}.pytest 2>&1 || { tail -30 ${out}.pytest; exit 1; }
-for B in 4096 8192; do for v in iter1 default; do
-  timeout -k 10 60 python tools/perf_kernel.py $v $B 20 >> $out 2>&1 || exit 1
-  for var in "$@"; do QLOCO_LIB=tools/_var/$var/libqloco.so timeout -k 10 60 python tools/perf_kernel.py $v $B 20 >> $out 2>&1 || exit 1; done
-done; done
-tail -1 ${out}.pytest; grep -v amdgpu.ids $out
+for b in $bs; do
+  N=$n GAIT=$gait timeout -k 10 120 python tools/perf_kernel.py default $b 5 >> $out 2>&1 || exit 1
+  for v in $vars; do
+    QLOCO_LIB=tools/_var/$v/libqloco.so N=$n GAIT=$gait timeout -k 10 120 python tools/perf_kernel.py default $b 5 >> $out 2>&1 || exit 1
+  done
+done
+grep -v amdgpu.ids $out

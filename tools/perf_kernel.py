@@ -21,8 +21,9 @@ VARIANTS = {
 name = sys.argv[1] if len(sys.argv) > 1 else "default"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
-N = 10
-x0, xr, ft, ct = srbd.generate(20261015, N, B, "trot")
+N = int(os.environ.get("N", 10))
+GAIT = os.environ.get("GAIT", "trot")
+x0, xr, ft, ct = srbd.generate(20261015, N, B, GAIT)
 dev = torch.device("cuda:0")
 args = [torch.from_numpy(a).to(dev) for a in (x0, xr, ft, ct)]
 legs = srbd.max_stance_legs(ct, N)
@@ -37,6 +38,8 @@ for _ in range(reps):
     s.solve(*args, out=out, max_legs=legs)
 e1.record()
 torch.cuda.synchronize()
-print("%-10s %-8s B=%6d  %9.1f us/launch  mean iters %.1f  rho_updates %.2f" % (
-    os.path.basename(os.path.dirname(os.environ.get("QLOCO_LIB", "/prod/x"))), name, B, e0.elapsed_time(e1) / reps * 1e3, out.iters.float().mean().item(),
-    out.rho_updates.float().mean().item()), flush=True)
+it = out.iters.float()
+print("%-10s %-6s N=%-2d %-8s B=%6d  %9.1f us/launch  iters mean %.1f p99 %d max %d  rho_updates mean %.2f max %d" % (
+    os.path.basename(os.path.dirname(os.environ.get("QLOCO_LIB", "/prod/x"))), GAIT, N, name, B,
+    e0.elapsed_time(e1) / reps * 1e3, it.mean().item(), int(it.quantile(0.99).item()), int(it.max().item()),
+    out.rho_updates.float().mean().item(), int(out.rho_updates.max().item())), flush=True)
