@@ -86,6 +86,8 @@ struct SrbdLds {
   f4v arz[NC];              // per var: scaled A entries (ra0, ra1, rz0, rz1) of its 2 slots
   float qs[NC];             // per var: scaled q
   int pair[NC];             // per var: 4*step + leg
+  int cst[NC];              // per var: step, kMaxN on padding (row of zeros in k0k2)
+  f2v k0k2[kMaxN * (kMaxN + 1)];  // [row step][col step]: horizon sums K0, K2
   float piv[2];
   float colv[W == 1 ? 1 : 2][W == 1 ? 1 : NC];  // W = 2 inverse: pivot column
   float red[W][16];
@@ -290,33 +292,44 @@ __device__ __forceinline__ PCoef p_coef(const SrbdLds<W> &S, f4v lo, f4v hi, int
   return c;
 }
 
-// Unscaled closed-form P row (padding rows: the identity row).
+// Unscaled closed-form P row (padding rows: the identity row).  Columns
+// come in leg triples (lanes 3l..3l+2 of a wave, lane 63 padding), so the
+// column component is static and K0 / K2 -- functions of the row and column
+// steps only -- are one LDS table read per triple.
 template <int W>
 __device__ __forceinline__ void gen_p_row(const SrbdLds<W> &S, const PCoef &pc, int t, bool valid,
-                                          int step, int comp, float Nf, float r2v, Row<W> &K) {
-  constexpr int NC = 64 * W;
+                                          int step, int comp, float r2v, Row<W> &K) {
   // opaque copies: keep LICM from hoisting per-column selects out of the ADMM loop
-  int tt = t, cp = comp;
-  float stf = (float)step;
+  int tt = t, kb = step * (kMaxN + 1);
   // padding lanes have zero coefficients, so only their diagonal needs a 1
   float dadd = valid ? r2v : 1.0f;
-  asm volatile("" : "+v"(tt), "+v"(cp), "+v"(stf), "+v"(dadd));
+  float lb0 = comp == 0 ? pc.linb : 0.0f, lb1 = comp == 1 ? pc.linb : 0.0f,
+        lb2 = comp == 2 ? pc.linb : 0.0f;
+  float le0 = comp == 0 ? pc.line : 0.0f, le1 = comp == 1 ? pc.line : 0.0f,
+        le2 = comp == 2 ? pc.line : 0.0f;
+  asm volatile("" : "+v"(tt), "+v"(kb), "+v"(dadd), "+v"(lb0), "+v"(lb1), "+v"(lb2), "+v"(le0),
+               "+v"(le1), "+v"(le2));
 #pragma unroll
-  for (int c4 = 0; c4 < NC; c4 += 4) {
-    __builtin_amdgcn_sched_barrier(0);  // bound live ranges: one 4-column group at a time
+  for (int h = 0; h < W; ++h) {
 #pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-      const int c = c4 + cc;
-      const f4v lo = S.bv[c][0], hi = S.bv[c][1];
-      float K0, K2;
-      k0k2(stf, hi.z, Nf, K0, K2);
-      const bool same = (float)cp == hi.w;
-      const float beta = pc.bq0 * lo.x + pc.bq1 * lo.y + pc.bq2 * lo.z + (same ? pc.linb : 0.0f);
-      const float epsv = pc.eq0 * lo.w + pc.eq1 * hi.x + pc.eq2 * hi.y + (same ? pc.line : 0.0f);
-      float pv = K0 * beta + K2 * epsv;
-      pv += (c == tt) ? dadd : 0.0f;
-      KE(K, c) = pv;
+    for (int l = 0; l < kLegsPerWave; ++l) {
+      __builtin_amdgcn_sched_barrier(0);  // bound live ranges: one triple at a time
+      const int c0 = 64 * h + 3 * l;
+      const f2v kk = S.k0k2[kb + S.cst[c0]];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int c = c0 + j;
+        const f4v lo = S.bv[c][0], hi = S.bv[c][1];
+        const float lb = j == 0 ? lb0 : (j == 1 ? lb1 : lb2);
+        const float le = j == 0 ? le0 : (j == 1 ? le1 : le2);
+        const float beta = fmaf(pc.bq2, lo.z, fmaf(pc.bq1, lo.y, fmaf(pc.bq0, lo.x, lb)));
+        const float epsv = fmaf(pc.eq2, hi.y, fmaf(pc.eq1, hi.x, fmaf(pc.eq0, lo.w, le)));
+        float pv = fmaf(kk.y, epsv, kk.x * beta);
+        pv += (c == tt) ? dadd : 0.0f;
+        KE(K, c) = pv;
+      }
     }
+    KE(K, 64 * h + 63) = (64 * h + 63 == tt) ? dadd : 0.0f;  // padding column
   }
 }
 
@@ -366,9 +379,11 @@ __device__ __forceinline__ float finalize_row(const SrbdLds<W> &S, int t, int cb
 // identity and never change.
 __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1> &K) {
   const int lane = t & 63;
+  int nc = __builtin_amdgcn_readfirstlane(ncol);
 #pragma unroll
   for (int k = 0; k < 64; ++k) {
-    if (k >= ncol) continue;  // wave-uniform; the loop stays fully unrolled (static register k)
+    asm volatile("" : "+s"(nc));  // the per-pivot compare stays a scalar one (not 64 hoisted masks)
+    if (k >= nc) continue;  // wave-uniform; the loop stays fully unrolled (static register k)
     const int buf = k & 1;
     float *bcf = reinterpret_cast<float *>(&S.bc[buf][0]);
     int tt = t;
@@ -396,9 +411,11 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1>
 template <int H>
 __device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, Row<2> &K) {
   const int lane = t & 63;
+  int nc = __builtin_amdgcn_readfirstlane(nw);
 #pragma unroll
   for (int kk = 0; kk < 64; ++kk) {
-    if (kk >= nw) continue;  // block-uniform
+    asm volatile("" : "+s"(nc));
+    if (kk >= nc) continue;  // block-uniform
     const int k = 64 * H + kk;
     const int buf = kk & 1;
     float *bcf = reinterpret_cast<float *>(&S.bc[buf][0]);
@@ -517,6 +534,13 @@ void srbd_admm_kernel(const SrbdArgs a) {
     const int pair = valid ? S.legtab[kLegsPerWave * wave + lslot] : 0;
     step = pair >> 2;
     leg = pair & 3;
+  }
+  S.cst[t] = valid ? step : kMaxN;
+  for (int idx = t; idx < N * (kMaxN + 1); idx += 64 * W) {
+    const int sr = idx / (kMaxN + 1), sc = idx - (kMaxN + 1) * sr;
+    float K0 = 0.0f, K2 = 0.0f;
+    if (sc < N) k0k2((float)sr, (float)sc, Nf, K0, K2);
+    S.k0k2[idx] = (f2v){K0, K2};
   }
 
   QL_PHASE(1);
@@ -703,7 +727,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
   // P row (closed form) and Ruiz equilibration, once
   {
     const PCoef pc = p_coef<W>(S, lo, hi, comp, valid, dtm, dt2m);
-    gen_p_row<W>(S, pc, t, valid, step, comp, Nf, r2v, K);
+    gen_p_row<W>(S, pc, t, valid, step, comp, r2v, K);
   }
   {
     {
@@ -714,6 +738,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
       float cnP = 0.0f;
 #pragma unroll
       for (int c = 0; c < NC; ++c) cnP = fmaxf(cnP, fabsf(KE(K, c)));
+      const float inv_n = 1.0f / (float)(n > 0 ? n : 1);
       for (int it = 0; it < a.scaling; ++it) {
         float cnA = fmaxf(fabsf(ra0), fabsf(ra1));
         const float zmax = fmaxf(fabsf(rz0), fabsf(rz1));
@@ -752,8 +777,9 @@ void srbd_admm_kernel(const SrbdArgs a) {
         const float sumP = bsum<W>(valid ? cn2 : 0.0f, S.red);
         float qm[1] = {valid ? fabsf(qv) : 0.0f};
         bmax<W, 1>(qm, S.red);
-        const float meanP = cs * sumP / (float)(n > 0 ? n : 1);
-        const float ctc = 1.0f / limit_scaling(fmaxf(meanP, limit_scaling(qm[0])));
+        const float meanP = cs * sumP * inv_n;
+        // v_rcp_f32 (1 ulp), like the rsq above: a heuristic factor
+        const float ctc = __builtin_amdgcn_rcpf(limit_scaling(fmaxf(meanP, limit_scaling(qm[0]))));
         qv *= ctc;
         cs *= ctc;
         cnP = cn2 * cs;
@@ -840,7 +866,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
         const float t1 = lane_prev(tz), t2 = lane_prev(t1);
         float rhs = fmaf(sigma, x, (aw.x + aw.y) - qv);
         rhs += (comp == 2) ? (t1 + t2) : 0.0f;
-        const int buf = iter & 1;
+        // one wave's LDS operations complete in order: W = 1 needs no double buffer
+        const int buf = W == 1 ? 0 : (iter & 1);
         reinterpret_cast<float *>(&S.bc[buf][0])[t] = rhs;
         bsync<W>();
         // x_tilde = K^-1 rhs: one 16-byte LDS chunk per lane, DPP row_newbcast
@@ -901,7 +928,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
     {
       const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
       const PCoef pc = p_coef<W>(S, blo, bhi, comp, valid, dtm, dt2m);
-      gen_p_row<W>(S, pc, t, valid, (int)bhi.z, comp, Nf, S.aux[0][t], K);
+      gen_p_row<W>(S, pc, t, valid, (int)bhi.z, comp, S.aux[0][t], K);
     }
   }
   if (status != QLOCO_OK) {  // max_iter reached (OSQP: solved inaccurate or max_iter)
