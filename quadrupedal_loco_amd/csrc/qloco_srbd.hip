@@ -32,6 +32,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "qloco_common.hpp"
 #include "qloco_dpp.inc"
 
@@ -187,23 +189,42 @@ __device__ __forceinline__ float bqp_t(const SrbdLds<W> &S, int step, int comp, 
   return acc;
 }
 
-// S.Wc[j][r] = sum_{i>=j} wt(i-j) S.err[i][r]; wt = 1 on b rows (6..11,
-// W0), (i-j) on e rows (0..5, W1).  Parallel over (j, r).
+// Per-row scans over the horizon, lanes r < 12 (one row each), the N
+// values read up front (unconditional in-bounds loads, one wait), the
+// recurrences in registers behind uniform step guards.
+//  forward (P x only): S.err[i][r] <- q2[r] * s_i[r], s_i = sum_{j<=i} agg_j
+//      on b rows (6..11), sum_{j<i} (i-j) agg_j on e rows (0..5);
+//  suffix: S.Wc[j][r] = sum_{i>=j} wt(i-j) S.err[i][r]; wt = 1 on b rows
+//      (W0), (i-j) on e rows (W1).
 template <int W>
-__device__ __forceinline__ void suffix_weights(SrbdLds<W> &S, int N) {
-  for (int idx = threadIdx.x; idx < 12 * N; idx += 64 * W) {
-    const int j = idx / 12, r = idx - 12 * j;
-    const bool brow = r >= 6;
-    float acc = 0.0f;
+__device__ __forceinline__ void row_scans(SrbdLds<W> &S, int N, bool forward) {
+  const int r = threadIdx.x;
+  if (r >= 12) return;
+  const bool brow = r >= 6;
+  float v[kMaxN];
+#pragma unroll
+  for (int i = 0; i < kMaxN; ++i) v[i] = S.err[12 * i + r];
+  if (forward) {
+    const float q = S.q2[r];
+    float pa = 0.0f, pe = 0.0f, se = 0.0f;
 #pragma unroll
     for (int i = 0; i < kMaxN; ++i) {
       if (i < N) {
-        const float e = S.err[12 * i + r];
-        const float wt = (i >= j) ? (brow ? 1.0f : (float)(i - j)) : 0.0f;
-        acc = fmaf(wt, e, acc);
+        se += pe;
+        pe += v[i];
+        pa += v[i];
+        v[i] = q * (brow ? pa : se);
       }
     }
-    S.Wc[idx] = acc;
+  }
+  float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+  for (int j = kMaxN - 1; j >= 0; --j) {
+    if (j < N) {
+      s1 += s0;  // S1[j] = S1[j+1] + S0[j+1]
+      s0 += v[j];
+      S.Wc[12 * j + r] = brow ? s0 : s1;
+    }
   }
 }
 
@@ -211,7 +232,7 @@ __device__ __forceinline__ void suffix_weights(SrbdLds<W> &S, int N) {
 // x, 0 on padding) and synced.  Three phases, all lanes busy:
 //  (a) per-step aggregates agg_j[s] = sum_{v in step j} Bcoef(v, s) x_v
 //  (b) state rows s_i (b rows: prefix sum, e rows: weighted prefix sum),
-//      w_i = Q s_i, suffix weights W0 / W1 per (j, r) -> S.Wc
+//      w_i = Q s_i, suffix weights W0 / W1 per (j, r) -> S.Wc (row_scans)
 //  (c) this lane's (Bqp' w)_v + R x_v
 template <int W>
 __device__ __forceinline__ float p_times_x(SrbdLds<W> &S, int N, bool valid, int step, int comp,
@@ -240,24 +261,7 @@ __device__ __forceinline__ float p_times_x(SrbdLds<W> &S, int N, bool valid, int
     S.err[idx] = acc;
   }
   bsync<W>();
-  for (int idx = t; idx < 12 * N; idx += 64 * W) {
-    const int jv = idx / 12, r = idx - 12 * jv;
-    const bool brow = r >= 6;
-    float pa = 0.0f, pe = 0.0f, se = 0.0f, acc = 0.0f;
-#pragma unroll
-    for (int i = 0; i < kMaxN; ++i) {
-      if (i < N) {
-        const float ag = S.err[12 * i + r];
-        se += pe;  // sum_{j<i} (i-j) agg_j
-        pe += ag;
-        pa += ag;
-        const float si = brow ? pa : se;
-        const float wt = (i >= jv) ? (brow ? 1.0f : (float)(i - jv)) : 0.0f;
-        acc = fmaf(wt, si, acc);
-      }
-    }
-    S.Wc[idx] = S.q2[r] * acc;
-  }
+  row_scans<W>(S, N, true);
   bsync<W>();
   return valid ? bqp_t<W>(S, step, comp, lo, hi, dtm, dt2m) + r2v * xu : 0.0f;
 }
@@ -339,11 +343,16 @@ __device__ __forceinline__ void gen_p_row(const SrbdLds<W> &S, const PCoef &pc, 
 // (pivot tracking of the W = 2 inverse).
 template <int W>
 __device__ __forceinline__ float finalize_row(const SrbdLds<W> &S, int t, int cbase, float rs,
-                                              float add0, float add1, float add2, Row<W> &K) {
+                                              float add0, float add1, float add2, bool c60,
+                                              Row<W> &K) {
   constexpr int NC = 64 * W;
   const int lane = t & 63;
   const f4v d0 = reinterpret_cast<const f4v *>(S.Dc)[lane & 15];
-  QL_DPP_MUL64(K.k, 0, d0);
+  if (W == 1 && c60) {  // padding columns 60..63 have D = 1
+    QL_DPP_MUL60(K.k, 0, d0);
+  } else {
+    QL_DPP_MUL64(K.k, 0, d0);
+  }
   if constexpr (W == 2) {
     const f4v d1 = reinterpret_cast<const f4v *>(S.Dc)[16 + (lane & 15)];
     QL_DPP_MUL64(K.k, 64, d1);
@@ -377,6 +386,7 @@ __device__ __forceinline__ float finalize_row(const SrbdLds<W> &S, int t, int cb
 // one coalesced ds_write_b32 and one ds_read_b128 per pivot, the row fanned
 // out by DPP.  Only the valid pivots run; padding rows / columns are the
 // identity and never change.
+template <bool C60>
 __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1> &K) {
   const int lane = t & 63;
   int nc = __builtin_amdgcn_readfirstlane(ncol);
@@ -399,7 +409,11 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1>
     const float pinv = __builtin_amdgcn_rcpf(p);
     const float g = (tt == k) ? (1.0f - pinv) : v * pinv;
     const float ng = -g;
-    QL_DPP_GJ64(K.k, 0, r0, ng);
+    if constexpr (C60) {
+      QL_DPP_GJ60(K.k, 0, r0, ng);
+    } else {
+      QL_DPP_GJ64(K.k, 0, r0, ng);
+    }
   }
   bsync<1>();
 }
@@ -526,6 +540,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
     lw = lw < 0 ? 0 : (lw > kLegsPerWave ? kLegsPerWave : lw);
     ncol[w] = 3 * lw;
   }
+  // every valid column below 60: the 60-column DPP forms (uniform)
+  const bool c60 = W == 1 && __builtin_amdgcn_readfirstlane(ncol[0]) <= 60;
   const int lslot = lane / 3;
   const int comp = lane - 3 * lslot;
   const bool valid = (lane < 63) && (kLegsPerWave * wave + lslot < nlegs);
@@ -620,7 +636,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
     S.err[idx] = S.q2[s] * (xf - a.xref[b * 13 * N + 13 * i + s]);
   }
   bsync<W>();
-  suffix_weights<W>(S, N);
+  row_scans<W>(S, N, false);
   bsync<W>();
   float qv = valid ? bqp_t<W>(S, step, comp, lo, hi, dtm, dt2m) : 0.0f;
 
@@ -765,7 +781,11 @@ void srbd_admm_kernel(const SrbdArgs a) {
         float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f, t0, t1, t2, t3;
         {
           const f4v d0 = S.bc[buf][lane & 15];
-          QL_DPP_ABSMAX64(m0, m1, m2, m3, t0, t1, t2, t3, d0, K.k, 0);
+          if (W == 1 && c60) {  // padding columns: K_rc = 0 on valid rows
+            QL_DPP_ABSMAX60(m0, m1, m2, m3, t0, t1, t2, t3, d0, K.k, 0);
+          } else {
+            QL_DPP_ABSMAX64(m0, m1, m2, m3, t0, t1, t2, t3, d0, K.k, 0);
+          }
           if constexpr (W == 2) {
             const f4v d1 = S.bc[buf][16 + (lane & 15)];
             QL_DPP_ABSMAX64(m0, m1, m2, m3, t0, t1, t2, t3, d1, K.k, 64);
@@ -814,11 +834,15 @@ void srbd_admm_kernel(const SrbdArgs a) {
     {
       float add0, add1, add2;
       leg_block(add0, add1, add2);
-      const float dg = finalize_row<W>(S, t, t - comp, cs * S.Dc[t], add0, add1, add2, K);
+      const float dg = finalize_row<W>(S, t, t - comp, cs * S.Dc[t], add0, add1, add2, c60, K);
       if (first) QL_PHASE(5);
       if constexpr (W == 1) {
         (void)dg;
-        invert_w1(S, t, ncol[0], K);
+        if (c60) {
+          invert_w1<true>(S, t, ncol[0], K);
+        } else {
+          invert_w1<false>(S, t, ncol[0], K);
+        }
       } else {
         (void)dg;
         invert_w2(S, t, ncol, K);
@@ -853,6 +877,10 @@ void srbd_admm_kernel(const SrbdArgs a) {
       const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
       const float qv = S.qs[t];
       const f2v rv = {RV0, rho}, rvi2 = {RVI0, rvi};
+      const float m2 = comp == 2 ? 1.0f : 0.0f;
+      // C60: n <= 60, columns 60..63 are identity padding (K^-1 entries 0)
+      auto run_block = [&](auto c60_tag) {
+      constexpr bool C60 = decltype(c60_tag)::value;
       for (; iter < next; ++iter) {
         // compiler-only barrier: LDS-resident tables (bv, Dc, zb, ...) are
         // re-read where used instead of being hoisted into loop-live registers
@@ -863,27 +891,49 @@ void srbd_admm_kernel(const SrbdArgs a) {
         const f2v w = __builtin_elementwise_fma(rv, z, -y);
         const f2v aw = ra * w, zw = rz * w;
         const float tz = zw.x + zw.y;
-        const float t1 = lane_prev(tz), t2 = lane_prev(t1);
         float rhs = fmaf(sigma, x, (aw.x + aw.y) - qv);
-        rhs += (comp == 2) ? (t1 + t2) : 0.0f;
+        // z lane: += tz[l-1] + tz[l-2] (its leg's x and y lanes), as two
+        // DPP-fused ops: u = tz[l-1] + tz[l], rhs += m2 * u[l-1]
+        {
+          float u;
+          asm("s_nop 1\n\t"
+              "v_add_f32_dpp %0, %2, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+              "s_nop 1\n\t"
+              "v_fmac_f32_dpp %1, %0, %3 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+              : "=&v"(u), "+v"(rhs)
+              : "v"(tz), "v"(m2));
+        }
         // one wave's LDS operations complete in order: W = 1 needs no double buffer
         const int buf = W == 1 ? 0 : (iter & 1);
         reinterpret_cast<float *>(&S.bc[buf][0])[t] = rhs;
         bsync<W>();
         // x_tilde = K^-1 rhs: one 16-byte LDS chunk per lane, DPP row_newbcast
         // fans it out to the register-resident row (qloco_dpp.inc)
-        float acc0, acc1, acc2, acc3;
+        float xt;
         {
           const f4v r0 = S.bc[buf][lane & 15];
-          QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r0, K.k, 0);
-          if constexpr (W == 2) {
-            const f4v r1 = S.bc[buf][16 + (lane & 15)];
-            QL_DPP_MATVEC64_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
+          if constexpr (W == 1) {  // two accumulator chains
+            float acc0, acc1;
+            if constexpr (C60) {
+              QL_DPP_MATVEC60_2(acc0, acc1, r0, K.k, 0);
+            } else {
+              QL_DPP_MATVEC64_2(acc0, acc1, r0, K.k, 0);
+            }
+            xt = acc0 + acc1;
+          } else {
+            float acc0, acc1, acc2, acc3;
+            QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r0, K.k, 0);
+            if constexpr (W == 2) {
+              const f4v r1 = S.bc[buf][16 + (lane & 15)];
+              QL_DPP_MATVEC64_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
+            }
+            xt = (acc0 + acc1) + (acc2 + acc3);
           }
         }
-        const float xt = (acc0 + acc1) + (acc2 + acc3);
+        // x / y lanes take their leg's z lane (2 / 1 lanes up); z lanes have
+        // rz = 0, so their pick is irrelevant
         const float n1 = lane_next(xt), n2 = lane_next(n1);
-        const float xtz = comp == 0 ? n2 : (comp == 1 ? n1 : xt);
+        const float xtz = comp == 0 ? n2 : n1;
         // update_x / update_z / update_y (relaxation alpha, projection on [l, u])
         x = fmaf(alpha, xt, oma * x);
         const f2v zt = __builtin_elementwise_fma(rz, (f2v)(xtz), ra * xt);
@@ -893,6 +943,12 @@ void srbd_admm_kernel(const SrbdArgs a) {
                         __builtin_amdgcn_fmed3f(v.y, bnd.z, bnd.w)};
         y = __builtin_elementwise_fma(rv, zr - zn, y);
         z = zn;
+      }
+      };
+      if (c60) {
+        run_block(std::true_type{});
+      } else {
+        run_block(std::false_type{});
       }
       const bool can_check = ctm && (iter % ctm == 0);
       const bool do_rho = interval && (iter % interval == 0);

@@ -45,34 +45,34 @@ def matvec(acc):
             "\\n\\t\" \\\n      \"".join(body) + "\" \\\n      : " + outs + " \\\n      : " + ins + ")\n")
 
 
-def gj():
+def gj(nch=16):
     # outputs KK[B+c] = %c (c < 64), inputs R.x..R.w = %64..%67, NG = %68
-    body = ["s_nop 4"] + [dpp(4 * j + e, 64 + e, 68, j) for j in range(16) for e in range(4)]
+    body = ["s_nop 4"] + [dpp(4 * j + e, 64 + e, 68, j) for j in range(nch) for e in range(4)]
     outs = ", ".join('"+v"((KK)[(B) + %d])' % c for c in range(64))
     ins = '"v"((R).x), "v"((R).y), "v"((R).z), "v"((R).w), "v"(NG)'
     return ("// KK[B + 4j + e] += R_e(lane j of the row) * NG\n"
-            "#define QL_DPP_GJ64(KK, B, R, NG) \\\n  asm(\"" +
+            "#define QL_DPP_GJ%d(KK, B, R, NG) \\\n  asm(\"" % (4 * nch) +
             "\\n\\t\" \\\n      \"".join(body) + "\" \\\n      : " + outs + " \\\n      : " + ins + ")\n")
 
 
-def mul():
+def mul(nch=16):
     # in/out KK[B+c] = %c, inputs R = %64..%67: KK[B+4j+e] *= R_e(lane j of the row)
     body = ["s_nop 4"] + ["v_mul_f32_dpp %%%d, %%%d, %%%d row_newbcast:%d row_mask:0xf bank_mask:0xf"
-                          % (4 * j + e, 64 + e, 4 * j + e, j) for j in range(16) for e in range(4)]
+                          % (4 * j + e, 64 + e, 4 * j + e, j) for j in range(nch) for e in range(4)]
     outs = ", ".join('"+v"((KK)[(B) + %d])' % c for c in range(64))
     ins = '"v"((R).x), "v"((R).y), "v"((R).z), "v"((R).w)'
     return ("// KK[B + 4j + e] *= R_e(lane j of the row)\n"
-            "#define QL_DPP_MUL64(KK, B, R) \\\n  asm(\"" +
+            "#define QL_DPP_MUL%d(KK, B, R) \\\n  asm(\"" % (4 * nch) +
             "\\n\\t\" \\\n      \"".join(body) + "\" \\\n      : " + outs + " \\\n      : " + ins + ")\n")
 
 
-def absmax():
+def absmax(nch=16):
     # outputs A0..A3 = %0..%3, temps T0..T3 = %4..%7 (early clobber),
     # inputs R = %8..%11, KK[B+c] = %12+c:  A_e = max(A_e, R_e(lane j) * |KK[B+4j+e]|)
     # two products per v_max3: 64 DPP multiplies + 32 max3 per 64 columns;
     # accumulators A0/A1 take the even / odd chunk halves, A2/A3 the next j
     body = ["s_nop 4"]
-    for j in range(16):
+    for j in range(nch):
         for e in range(4):
             body.append("v_mul_f32_dpp %%%d, %%%d, |%%%d| row_newbcast:%d row_mask:0xf bank_mask:0xf"
                         % (4 + e, 8 + e, 12 + 4 * j + e, j))
@@ -83,7 +83,26 @@ def absmax():
     ins = ", ".join(['"v"((R).x)', '"v"((R).y)', '"v"((R).z)', '"v"((R).w)'] +
                     ['"v"((KK)[(B) + %d])' % c for c in range(64)])
     return ("// A_e = max(A_e, R_e(lane j of the row) * |KK[B + 4j + e]|); T0..T3 scratch\n"
-            "#define QL_DPP_ABSMAX64(A0, A1, A2, A3, T0, T1, T2, T3, R, KK, B) \\\n  asm(\"" +
+            "#define QL_DPP_ABSMAX%d(A0, A1, A2, A3, T0, T1, T2, T3, R, KK, B) \\\n  asm(\"" % (4 * nch) +
+            "\\n\\t\" \\\n      \"".join(body) + "\" \\\n      : " + outs + " \\\n      : " + ins + ")\n")
+
+
+def matvec2(nch=16):
+    # two accumulators (A0: components x,z; A1: y,w): outputs %0,%1, R = %2..%5, KK = %6+c
+    body = ["s_nop 1"]
+    for j in range(nch):
+        for e in range(4):
+            a = e % 2
+            if j == 0 and e < 2:
+                body.append("v_mul_f32_dpp %%%d, %%%d, %%%d row_newbcast:0 row_mask:0xf bank_mask:0xf"
+                            % (a, 2 + e, 6 + e))
+            else:
+                body.append(dpp(a, 2 + e, 6 + 4 * j + e, j))
+    outs = '"=&v"(A0), "=&v"(A1)'
+    ins = ", ".join(['"v"((R).x)', '"v"((R).y)', '"v"((R).z)', '"v"((R).w)'] +
+                    ['"v"((KK)[(B) + %d])' % c for c in range(64)])
+    return ("// A0 + A1 = sum_j,e KK[B + 4j + e] * R_e(lane j of the row), two accumulators\n"
+            "#define QL_DPP_MATVEC%d_2(A0, A1, R, KK, B) \\\n  asm(\"" % (4 * nch) +
             "\\n\\t\" \\\n      \"".join(body) + "\" \\\n      : " + outs + " \\\n      : " + ins + ")\n")
 
 
@@ -91,5 +110,8 @@ if __name__ == "__main__":
     with open(OUT, "w") as f:
         f.write("// Generated by tools/gen_dpp_asm.py -- do not edit.\n#pragma once\n\n")
         f.write(matvec(False) + "\n" + matvec(True) + "\n" + gj() + "\n" + mul() + "\n" +
-                absmax())
+                absmax() + "\n" + matvec2() + "\n" +
+                # 60-column forms: n <= 60 (every N = 10 trot / pace instance) --
+                # columns 60..63 are identity padding, their updates are zero
+                gj(15) + "\n" + mul(15) + "\n" + absmax(15) + "\n" + matvec2(15))
     print(OUT)
