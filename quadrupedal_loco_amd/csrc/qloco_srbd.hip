@@ -744,6 +744,10 @@ void srbd_admm_kernel(const SrbdArgs a) {
   {
     const PCoef pc = p_coef<W>(S, lo, hi, comp, valid, dtm, dt2m);
     gen_p_row<W>(S, pc, t, valid, step, comp, r2v, K);
+#ifdef QLOCO_ABLATE_DUP_GENP  // timing experiments only (tools/variant_lib.py)
+    asm volatile("" ::: "memory");
+    gen_p_row<W>(S, pc, t, valid, step, comp, r2v, K);
+#endif
   }
   {
     {
@@ -840,6 +844,10 @@ void srbd_admm_kernel(const SrbdArgs a) {
         (void)dg;
         if (c60) {
           invert_w1<true>(S, t, ncol[0], K);
+#ifdef QLOCO_ABLATE_DUP_INV  // timing experiments only: K^-1 -> K -> K^-1
+          invert_w1<true>(S, t, ncol[0], K);
+          invert_w1<true>(S, t, ncol[0], K);
+#endif
         } else {
           invert_w1<false>(S, t, ncol[0], K);
         }

@@ -46,23 +46,25 @@ def matvec(acc):
 
 
 def gj(nch=16):
-    # outputs KK[B+c] = %c (c < 64), inputs R.x..R.w = %64..%67, NG = %68
-    body = ["s_nop 4"] + [dpp(4 * j + e, 64 + e, 68, j) for j in range(nch) for e in range(4)]
-    outs = ", ".join('"+v"((KK)[(B) + %d])' % c for c in range(64))
+    # outputs KK[B+c] = %c (c < 4 nch), inputs R.x..R.w = %nc..%nc+3, NG = %nc+4
+    nc = 4 * nch
+    body = ["s_nop 4"] + [dpp(4 * j + e, nc + e, nc + 4, j) for j in range(nch) for e in range(4)]
+    outs = ", ".join('"+v"((KK)[(B) + %d])' % c for c in range(nc))
     ins = '"v"((R).x), "v"((R).y), "v"((R).z), "v"((R).w), "v"(NG)'
-    return ("// KK[B + 4j + e] += R_e(lane j of the row) * NG\n"
-            "#define QL_DPP_GJ%d(KK, B, R, NG) \\\n  asm(\"" % (4 * nch) +
+    return ("// KK[B + 4j + e] += R_e(lane j of the row) * NG, columns < %d\n" % nc +
+            "#define QL_DPP_GJ%d(KK, B, R, NG) \\\n  asm(\"" % nc +
             "\\n\\t\" \\\n      \"".join(body) + "\" \\\n      : " + outs + " \\\n      : " + ins + ")\n")
 
 
 def mul(nch=16):
-    # in/out KK[B+c] = %c, inputs R = %64..%67: KK[B+4j+e] *= R_e(lane j of the row)
+    # in/out KK[B+c] = %c (c < 4 nch), inputs R = %nc..%nc+3: KK[B+4j+e] *= R_e(lane j)
+    nc = 4 * nch
     body = ["s_nop 4"] + ["v_mul_f32_dpp %%%d, %%%d, %%%d row_newbcast:%d row_mask:0xf bank_mask:0xf"
-                          % (4 * j + e, 64 + e, 4 * j + e, j) for j in range(nch) for e in range(4)]
-    outs = ", ".join('"+v"((KK)[(B) + %d])' % c for c in range(64))
+                          % (4 * j + e, nc + e, 4 * j + e, j) for j in range(nch) for e in range(4)]
+    outs = ", ".join('"+v"((KK)[(B) + %d])' % c for c in range(nc))
     ins = '"v"((R).x), "v"((R).y), "v"((R).z), "v"((R).w)'
-    return ("// KK[B + 4j + e] *= R_e(lane j of the row)\n"
-            "#define QL_DPP_MUL%d(KK, B, R) \\\n  asm(\"" % (4 * nch) +
+    return ("// KK[B + 4j + e] *= R_e(lane j of the row), columns < %d\n" % nc +
+            "#define QL_DPP_MUL%d(KK, B, R) \\\n  asm(\"" % nc +
             "\\n\\t\" \\\n      \"".join(body) + "\" \\\n      : " + outs + " \\\n      : " + ins + ")\n")
 
 
@@ -81,7 +83,7 @@ def absmax(nch=16):
         body.append("v_max3_f32 %%%d, %%%d, %%6, %%7" % (a1, a1))
     outs = ", ".join(['"+v"(A%d)' % e for e in range(4)] + ['"=&v"(T%d)' % e for e in range(4)])
     ins = ", ".join(['"v"((R).x)', '"v"((R).y)', '"v"((R).z)', '"v"((R).w)'] +
-                    ['"v"((KK)[(B) + %d])' % c for c in range(64)])
+                    ['"v"((KK)[(B) + %d])' % c for c in range(4 * nch)])
     return ("// A_e = max(A_e, R_e(lane j of the row) * |KK[B + 4j + e]|); T0..T3 scratch\n"
             "#define QL_DPP_ABSMAX%d(A0, A1, A2, A3, T0, T1, T2, T3, R, KK, B) \\\n  asm(\"" % (4 * nch) +
             "\\n\\t\" \\\n      \"".join(body) + "\" \\\n      : " + outs + " \\\n      : " + ins + ")\n")
@@ -100,7 +102,7 @@ def matvec2(nch=16):
                 body.append(dpp(a, 2 + e, 6 + 4 * j + e, j))
     outs = '"=&v"(A0), "=&v"(A1)'
     ins = ", ".join(['"v"((R).x)', '"v"((R).y)', '"v"((R).z)', '"v"((R).w)'] +
-                    ['"v"((KK)[(B) + %d])' % c for c in range(64)])
+                    ['"v"((KK)[(B) + %d])' % c for c in range(4 * nch)])
     return ("// A0 + A1 = sum_j,e KK[B + 4j + e] * R_e(lane j of the row), two accumulators\n"
             "#define QL_DPP_MATVEC%d_2(A0, A1, R, KK, B) \\\n  asm(\"" % (4 * nch) +
             "\\n\\t\" \\\n      \"".join(body) + "\" \\\n      : " + outs + " \\\n      : " + ins + ")\n")

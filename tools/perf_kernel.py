@@ -14,6 +14,8 @@ if os.environ.get("QLOCO_LIB"):  # experimental variant (tools/variant_lib.py)
 VARIANTS = {
     "default": {},
     "iter1": dict(max_iter=1, check_termination=0, adaptive_rho=0),
+    "iter1s20": dict(max_iter=1, check_termination=0, adaptive_rho=0, scaling=20),
+    "iter1s0": dict(max_iter=1, check_termination=0, adaptive_rho=0, scaling=0),
     "iter150": dict(max_iter=150, check_termination=0, adaptive_rho=0),
     "rho25": dict(max_iter=150, eps_abs=1e-12, eps_rel=1e-12, adaptive_rho=1,
                   adaptive_rho_interval=25, adaptive_rho_tolerance=1.0),
