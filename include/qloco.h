@@ -215,6 +215,27 @@ int qloco_body_mpc_step(int64_t batch, const int32_t *i, const double *bodyangle
 /* PRMPCClass::Indexfind (PRMPCClass.cpp:716-738) on B fp64 times -> int32 */
 int qloco_body_indexfind(int64_t batch, const double *t, int32_t *j_period, void *stream);
 
+/* ====================================================================== */
+/* 5. Go1 leg kinematics, batched (fp64, one leg per lane)                  */
+/*    replaces Kinematicclass (go1_rt_control/src/kinematics/Kinematics.cpp) */
+/*    called per leg at servo.cpp:734-741 (FK_g + Jacobian_kin) and         */
+/*    servo.cpp:1038-1051 (IK_g + Jacobian_kin)                             */
+/* ====================================================================== */
+/* Forward_kinematics (:63-142, body_p = body_r = NULL: hip frame) or
+ * Forward_kinematics_g (:145-229; body_p[n*3], body_r[n*3] = roll, pitch,
+ * yaw).  q[n*3] (hip, thigh, calf), leg[n] (0 FR, 1 FL, 2 RR, 3 RL)
+ * -> pos[n*3], jac[n*9] (Jacobian_kin, 3x3 column-major; may be NULL). */
+int qloco_leg_fk(int64_t n, const double *q, const int32_t *leg, const double *body_p,
+                 const double *body_r, double *pos, double *jac, void *stream);
+/* Inverse_kinematics (:233-267, 10 damped Newton steps, lamda 0.5) or
+ * Inverse_kinematics_g (:270-304, 15 steps) from q_ini[n*3] toward
+ * pos_des[n*3] -> q_out[n*3]; optional pos[n*3] / jac[n*9] at q_out (the
+ * reference's pos_cal / Jacobian_kin after the call) and updates[n] (Newton
+ * steps applied).  Reference stop tests reproduced as written. */
+int qloco_leg_ik(int64_t n, const double *pos_des, const double *q_ini, const int32_t *leg,
+                 const double *body_p, const double *body_r, double *q_out, double *pos,
+                 double *jac, int32_t *updates, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

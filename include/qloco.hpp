@@ -18,6 +18,8 @@
  *                                    (PRMPCClass.h:69-71; gait_fast.cpp:620)
  *   ConvexMpcBatch                <- A1RobotControl::compute_grf MPC branch +
  *                                    ConvexMpc (A1RobotControl.cpp:452-600)
+ *   Kinematicclass                <- go1_rt_control Kinematicclass
+ *                                    (Kinematics.h:30-61; servo.cpp:734-741, :1038-1051)
  *
  * Every class is batched over B independent robots (B = 1 is the drop-in
  * case).  Host arrays are staged to the device on the object's HIP stream;
@@ -205,6 +207,44 @@ class ConvexMpcBatch {
   float *d_x0_, *d_xr_, *d_feet_, *d_u0_;
   uint8_t *d_ct_;
   int32_t *d_st_, *d_it_;
+};
+
+
+// ------------------------------------------------------------------------
+// Kinematicclass (go1_rt_control/src/kinematics/Kinematics.h:30-61).  The
+// per-leg methods keep the reference's signatures and leave the Jacobian of
+// the last evaluation in Jacobian_kin (3x3 col-major), as the servo reads it
+// (servo.cpp:735, :1039); the batch methods run n legs in one launch and are
+// the intended use on the GPU (one leg per call is a host<->device round trip).
+// feet_flag: 0 FR, 1 FL, 2 RR, 3 RL.  body_R = (roll, pitch, yaw).
+class Kinematicclass {
+ public:
+  explicit Kinematicclass(int max_legs = 4);
+  std::array<double, 3> Forward_kinematics(const double q_joint[3], int feet_flag);
+  std::array<double, 3> Forward_kinematics_g(const double body_P[3], const double body_R[3],
+                                             const double q_joint[3], int feet_flag);
+  std::array<double, 3> Inverse_kinematics(const double pos_des[3], const double q_ini[3],
+                                           int feet_flag);
+  std::array<double, 3> Inverse_kinematics_g(const double body_P[3], const double body_R[3],
+                                             const double pos_des[3], const double q_ini[3],
+                                             int feet_flag);
+  // n legs (host arrays, row layout of qloco_leg_fk / qloco_leg_ik); body_p /
+  // body_r both NULL for the hip frame.  jac / pos_out / updates may be NULL.
+  void forward_batch(int n, const double *q, const int32_t *leg, const double *body_p,
+                     const double *body_r, double *pos, double *jac);
+  void inverse_batch(int n, const double *pos_des, const double *q_ini, const int32_t *leg,
+                     const double *body_p, const double *body_r, double *q_out, double *pos_out,
+                     double *jac, int32_t *updates);
+  std::array<double, 9> Jacobian_kin{};  // after the last per-leg call
+  std::array<double, 3> pos_cal{};       // FK at the last IK result (the reference's pos_cal)
+  int last_updates = 0;                  // Newton steps of the last per-leg IK
+
+ private:
+  int cap_;
+  DeviceArena arena_;
+  double *d_a_, *d_b_, *d_p_, *d_r_, *d_q_, *d_pos_, *d_jac_;
+  int32_t *d_leg_, *d_upd_;
+  void ensure(int n);
 };
 
 }  // namespace qloco

@@ -227,6 +227,27 @@ int qo_srbd_batch(const qo_srbd_spec *sp, const qo_admm_settings *st, int solver
                   double *u, int *iters, int *status, double *obj, int nthreads,
                   double *seconds);
 
+
+/* ------------------------------------------------------------------ */
+/* Go1 leg kinematics: go1_rt_control/src/kinematics/Kinematics.cpp     */
+/* (kinematics.c).  flag 0 FR, 1 FL, 2 RR, 3 RL; J 3x3 col-major.        */
+/* ------------------------------------------------------------------ */
+/* Forward_kinematics :63-142 (hip frame) */
+void qo_leg_fk(const double q[3], int flag, double pos[3], double J[9]);
+/* Forward_kinematics_g :145-229 (world frame; body_R = roll, pitch, yaw) */
+void qo_leg_fk_g(const double body_P[3], const double body_R[3], const double q[3], int flag,
+                 double pos[3], double J[9]);
+/* Inverse_kinematics :233-267 (body_P = body_R = NULL) or
+ * Inverse_kinematics_g :270-304.  Returns the number of Newton updates. */
+int qo_leg_ik(const double *body_P, const double *body_R, const double pos_des[3],
+              const double q_ini[3], int flag, double q_des[3], double pos[3], double J[9]);
+/* batch drivers (CPU baseline), row layout of qloco_leg_fk / qloco_leg_ik */
+void qo_leg_fk_batch(int64_t n, const double *q, const int32_t *leg, const double *body_p,
+                     const double *body_r, double *pos, double *J);
+void qo_leg_ik_batch(int64_t n, const double *pos_des, const double *q_ini, const int32_t *leg,
+                     const double *body_p, const double *body_r, double *q, double *pos, double *J,
+                     int32_t *updates);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,8 @@ SIGNATURES = {
     "qloco_max_gi_vars": (C.c_int, []),
     "qloco_force_params_default": (None, [C.POINTER(ForceParams)]),
     "qloco_force_qp_solve": (C.c_int, [C.POINTER(ForceParams), i64] + [vp] * 18),
+    "qloco_leg_fk": (C.c_int, [i64] + [vp] * 7),
+    "qloco_leg_ik": (C.c_int, [i64] + [vp] * 10),
     "qloco_joint_torques": (C.c_int, [i64] + [vp] * 9),
     "qloco_body_state_init_host": (C.c_int, [i64, vp]),
     "qloco_body_mpc_step": (C.c_int, [i64] + [vp] * 10),

@@ -436,4 +436,120 @@ void ConvexMpcBatch::compute_grf(const A1MpcState *s, double *forces) {
     }
 }
 
+
+// ------------------------------------------------------------------------
+// Kinematicclass -> qloco_leg_fk / qloco_leg_ik
+Kinematicclass::Kinematicclass(int max_legs) : cap_(0) {
+  if (max_legs < 1) throw Error("Kinematicclass: max_legs < 1", QLOCO_ERR_ARG);
+  ensure(max_legs);
+}
+
+void Kinematicclass::ensure(int n) {
+  if (n <= cap_) return;
+  const size_t N = n;
+  d_a_ = dalloc<double>(arena_, N * 3);
+  d_b_ = dalloc<double>(arena_, N * 3);
+  d_p_ = dalloc<double>(arena_, N * 3);
+  d_r_ = dalloc<double>(arena_, N * 3);
+  d_q_ = dalloc<double>(arena_, N * 3);
+  d_pos_ = dalloc<double>(arena_, N * 3);
+  d_jac_ = dalloc<double>(arena_, N * 9);
+  d_leg_ = dalloc<int32_t>(arena_, N);
+  d_upd_ = dalloc<int32_t>(arena_, N);
+  cap_ = n;
+}
+
+void Kinematicclass::forward_batch(int n, const double *q, const int32_t *leg,
+                                   const double *body_p, const double *body_r, double *pos,
+                                   double *jac) {
+  if (n < 0 || (n > 0 && (!q || !leg || !pos)) || ((body_p == nullptr) != (body_r == nullptr)))
+    throw Error("Kinematicclass::forward_batch: bad arguments", QLOCO_ERR_ARG);
+  if (n == 0) return;
+  ensure(n);
+  const size_t N = n;
+  const bool g = body_p != nullptr;
+  arena_.upload(d_q_, q, sizeof(double) * N * 3);
+  arena_.upload(d_leg_, leg, sizeof(int32_t) * N);
+  if (g) {
+    arena_.upload(d_p_, body_p, sizeof(double) * N * 3);
+    arena_.upload(d_r_, body_r, sizeof(double) * N * 3);
+  }
+  abi_ok(qloco_leg_fk(n, d_q_, d_leg_, g ? d_p_ : nullptr, g ? d_r_ : nullptr, d_pos_,
+                      jac ? d_jac_ : nullptr, arena_.stream()),
+         "qloco_leg_fk");
+  arena_.download(pos, d_pos_, sizeof(double) * N * 3);
+  if (jac) arena_.download(jac, d_jac_, sizeof(double) * N * 9);
+  arena_.sync();
+}
+
+void Kinematicclass::inverse_batch(int n, const double *pos_des, const double *q_ini,
+                                   const int32_t *leg, const double *body_p,
+                                   const double *body_r, double *q_out, double *pos_out,
+                                   double *jac, int32_t *updates) {
+  if (n < 0 || (n > 0 && (!pos_des || !q_ini || !leg || !q_out)) ||
+      ((body_p == nullptr) != (body_r == nullptr)))
+    throw Error("Kinematicclass::inverse_batch: bad arguments", QLOCO_ERR_ARG);
+  if (n == 0) return;
+  ensure(n);
+  const size_t N = n;
+  const bool g = body_p != nullptr;
+  arena_.upload(d_a_, pos_des, sizeof(double) * N * 3);
+  arena_.upload(d_b_, q_ini, sizeof(double) * N * 3);
+  arena_.upload(d_leg_, leg, sizeof(int32_t) * N);
+  if (g) {
+    arena_.upload(d_p_, body_p, sizeof(double) * N * 3);
+    arena_.upload(d_r_, body_r, sizeof(double) * N * 3);
+  }
+  abi_ok(qloco_leg_ik(n, d_a_, d_b_, d_leg_, g ? d_p_ : nullptr, g ? d_r_ : nullptr, d_q_, d_pos_,
+                      d_jac_, d_upd_, arena_.stream()),
+         "qloco_leg_ik");
+  arena_.download(q_out, d_q_, sizeof(double) * N * 3);
+  if (pos_out) arena_.download(pos_out, d_pos_, sizeof(double) * N * 3);
+  if (jac) arena_.download(jac, d_jac_, sizeof(double) * N * 9);
+  if (updates) arena_.download(updates, d_upd_, sizeof(int32_t) * N);
+  arena_.sync();
+}
+
+std::array<double, 3> Kinematicclass::Forward_kinematics(const double q_joint[3], int feet_flag) {
+  std::array<double, 3> p{};
+  const int32_t leg = feet_flag;
+  forward_batch(1, q_joint, &leg, nullptr, nullptr, p.data(), Jacobian_kin.data());
+  return p;
+}
+
+std::array<double, 3> Kinematicclass::Forward_kinematics_g(const double body_P[3],
+                                                           const double body_R[3],
+                                                           const double q_joint[3],
+                                                           int feet_flag) {
+  std::array<double, 3> p{};
+  const int32_t leg = feet_flag;
+  forward_batch(1, q_joint, &leg, body_P, body_R, p.data(), Jacobian_kin.data());
+  return p;
+}
+
+std::array<double, 3> Kinematicclass::Inverse_kinematics(const double pos_des[3],
+                                                         const double q_ini[3], int feet_flag) {
+  std::array<double, 3> q{};
+  const int32_t leg = feet_flag;
+  int32_t upd = 0;
+  inverse_batch(1, pos_des, q_ini, &leg, nullptr, nullptr, q.data(), pos_cal.data(),
+                Jacobian_kin.data(), &upd);
+  last_updates = upd;
+  return q;
+}
+
+std::array<double, 3> Kinematicclass::Inverse_kinematics_g(const double body_P[3],
+                                                           const double body_R[3],
+                                                           const double pos_des[3],
+                                                           const double q_ini[3],
+                                                           int feet_flag) {
+  std::array<double, 3> q{};
+  const int32_t leg = feet_flag;
+  int32_t upd = 0;
+  inverse_batch(1, pos_des, q_ini, &leg, body_P, body_R, q.data(), pos_cal.data(),
+                Jacobian_kin.data(), &upd);
+  last_updates = upd;
+  return q;
+}
+
 }  // namespace qloco

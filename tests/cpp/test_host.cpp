@@ -210,12 +210,61 @@ static void test_convex_mpc() {
               mpc.iters[0]);
 }
 
+// Kinematicclass: per-leg calls (servo.cpp:734-741 / :1038-1051 pattern)
+// and a batch, against the C restatement (oracle/kinematics.c).
+static void test_kinematics() {
+  qloco::Kinematicclass kin(256);
+  const double P[3] = {0.1, -0.2, 0.3}, E[3] = {0.05, -0.08, 1.2};
+  const double home[3] = {0.0, 0.87, -1.5};
+  for (int f = 0; f < 4; ++f) {
+    double po[3], Jo[9];
+    std::array<double, 3> p = kin.Forward_kinematics_g(P, E, home, f);
+    qo_leg_fk_g(P, E, home, f, po, Jo);
+    for (int r = 0; r < 3; ++r) CHECK(std::fabs(p[r] - po[r]) < 1e-12, "FK_g leg %d [%d]", f, r);
+    for (int r = 0; r < 9; ++r)
+      CHECK(std::fabs(kin.Jacobian_kin[r] - Jo[r]) < 1e-12, "Jacobian_kin leg %d [%d]", f, r);
+    // IK_g back to a perturbed target from the homing pose
+    const double qt[3] = {0.1, 0.8, -1.4};
+    double target[3], Jt[9];
+    qo_leg_fk_g(P, E, qt, f, target, Jt);
+    std::array<double, 3> q = kin.Inverse_kinematics_g(P, E, target, home, f);
+    double qo[3], pos_o[3], Jq[9];
+    const int n = qo_leg_ik(P, E, target, home, f, qo, pos_o, Jq);
+    CHECK(kin.last_updates == n, "IK_g updates %d vs %d", kin.last_updates, n);
+    for (int r = 0; r < 3; ++r) CHECK(std::fabs(q[r] - qo[r]) < 1e-9, "IK_g leg %d q[%d]", f, r);
+    // hip-frame IK (10 steps, signed-max stop)
+    q = kin.Inverse_kinematics(target, home, f);
+    const int nl = qo_leg_ik(nullptr, nullptr, target, home, f, qo, pos_o, Jq);
+    CHECK(kin.last_updates == nl, "IK updates %d vs %d", kin.last_updates, nl);
+    for (int r = 0; r < 3; ++r) CHECK(std::fabs(q[r] - qo[r]) < 1e-9, "IK leg %d q[%d]", f, r);
+  }
+  // batch of 256 legs, hip frame
+  const int n = 256;
+  std::vector<double> q(3 * n), pos(3 * n), J(9 * n);
+  std::vector<int32_t> leg(n);
+  for (int i = 0; i < n; ++i) {
+    leg[i] = i % 4;
+    q[3 * i] = 0.3 * std::sin(0.1 * i);
+    q[3 * i + 1] = 0.9 + 0.3 * std::cos(0.07 * i);
+    q[3 * i + 2] = -1.6 + 0.4 * std::sin(0.05 * i);
+  }
+  kin.forward_batch(n, q.data(), leg.data(), nullptr, nullptr, pos.data(), J.data());
+  for (int i = 0; i < n; ++i) {
+    double po[3], Jo[9];
+    qo_leg_fk(&q[3 * i], leg[i], po, Jo);
+    for (int r = 0; r < 3; ++r) CHECK(std::fabs(pos[3 * i + r] - po[r]) < 1e-12, "FK batch %d", i);
+    for (int r = 0; r < 9; ++r) CHECK(std::fabs(J[9 * i + r] - Jo[r]) < 1e-12, "J batch %d", i);
+  }
+  std::printf("kinematics ok: FK/IK per leg + batch of %d\n", n);
+}
+
 int main() {
   try {
     test_force_qp();
     test_qpsolver();
     test_body_mpc();
     test_convex_mpc();
+    test_kinematics();
   } catch (const qloco::Error &e) {
     std::printf("FAIL: qloco::Error %s (status %d)\n", e.what(), e.status);
     return 2;

@@ -133,6 +133,12 @@ def lib():
         L.qo_body_free.argtypes = [C.POINTER(BodyState)]
         L.qo_body_indexfind.restype = C.c_int
         L.qo_body_indexfind.argtypes = [C.POINTER(BodyState), C.c_double]
+        L.qo_leg_fk.argtypes = [dp, C.c_int, dp, dp]
+        L.qo_leg_fk_g.argtypes = [dp, dp, dp, C.c_int, dp, dp]
+        L.qo_leg_ik.restype = C.c_int
+        L.qo_leg_ik.argtypes = [dp, dp, dp, dp, C.c_int, dp, dp, dp]
+        L.qo_leg_fk_batch.argtypes = [C.c_int64] + [C.c_void_p] * 6
+        L.qo_leg_ik_batch.argtypes = [C.c_int64] + [C.c_void_p] * 9
         L.qo_body_theta_mpc.restype = C.c_int
         L.qo_body_theta_mpc.argtypes = [C.POINTER(BodyState), C.c_int, dp, dp, dp, dp, dp,
                                         dp, dp, dp, ip]
@@ -235,3 +241,28 @@ def exact_solve(H, g, A, l, u):
     u = np.ascontiguousarray(u, np.float64)
     st = lib().qo_exact_solve(n, m, P(Hc), P(g), P(Ac), P(l), P(u), P(x), C.byref(it))
     return x, st, it.value
+
+
+def leg_fk(q, flag, body_p=None, body_r=None):
+    """Kinematics.cpp Forward_kinematics(_g) restatement: (pos[3], J[9] col-major)."""
+    q = np.ascontiguousarray(q, np.float64)
+    pos = np.zeros(3)
+    J = np.zeros(9)
+    if body_p is None:
+        lib().qo_leg_fk(P(q), int(flag), P(pos), P(J))
+    else:
+        lib().qo_leg_fk_g(P(np.ascontiguousarray(body_p, np.float64)),
+                          P(np.ascontiguousarray(body_r, np.float64)), P(q), int(flag), P(pos), P(J))
+    return pos, J
+
+
+def leg_ik(pos_des, q_ini, flag, body_p=None, body_r=None):
+    """Inverse_kinematics(_g) restatement: (q[3], pos[3], J[9], newton updates)."""
+    q = np.zeros(3)
+    pos = np.zeros(3)
+    J = np.zeros(9)
+    bp = None if body_p is None else P(np.ascontiguousarray(body_p, np.float64))
+    br = None if body_r is None else P(np.ascontiguousarray(body_r, np.float64))
+    n = lib().qo_leg_ik(bp, br, P(np.ascontiguousarray(pos_des, np.float64)),
+                        P(np.ascontiguousarray(q_ini, np.float64)), int(flag), P(q), P(pos), P(J))
+    return q, pos, J, n

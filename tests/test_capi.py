@@ -145,5 +145,7 @@ def test_cpp_shim_exports_reference_classes():
     for sym in ("qloco::Dynamiccclass::force_distribution", "qloco::Dynamiccclass::force_opt",
                 "qloco::PRMPCClass::body_theta_mpc", "qloco::PRMPCClass::Indexfind",
                 "qloco::QPsolverGpu::resize", "qloco::QPsolverGpu::solve",
-                "qloco::QPBaseClassGpu::solveQP", "qloco::ConvexMpcBatch::compute_grf"):
+                "qloco::QPBaseClassGpu::solveQP", "qloco::ConvexMpcBatch::compute_grf",
+                "qloco::Kinematicclass::Forward_kinematics_g",
+                "qloco::Kinematicclass::Inverse_kinematics_g"):
         assert sym in out, sym

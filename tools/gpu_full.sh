@@ -14,3 +14,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $out/pmc_fetch -o
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $out/pmc_write -o run -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline > $out/pmc_write.log 2>&1 || { tail -20 $out/pmc_write.log; exit 1; }
 tail -2 $out/pytest_gpu.log; tail -1 $out/smoke.log; cat $out/bench.json
 find $out/ktrace -name "*.csv"
+# §8f row 4: leg kinematics bench + kernel trace
+timeout -k 10 300 python tools/bench_kin.py > $out/bench_kin.json 2> $out/bench_kin.err || { tail -20 $out/bench_kin.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $out/ktrace_kin -o run -- python tools/bench_kin.py --no-cpu-baseline > $out/ktrace_kin.log 2>&1 || { tail -20 $out/ktrace_kin.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $out/pmc_kin_fetch -o run -- python tools/bench_kin.py --no-cpu-baseline --steps 10 > $out/pmc_kin_fetch.log 2>&1 || { tail -20 $out/pmc_kin_fetch.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $out/pmc_kin_write -o run -- python tools/bench_kin.py --no-cpu-baseline --steps 10 > $out/pmc_kin_write.log 2>&1 || { tail -20 $out/pmc_kin_write.log; exit 1; }
+cat $out/bench_kin.json
