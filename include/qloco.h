@@ -104,10 +104,12 @@ int qloco_srbd_solve(const qloco_srbd_spec *spec, int64_t batch, const float *x0
 
 /* Extended form of qloco_srbd_solve: additionally returns rho_updates[B]
  * (number of adaptive-rho refactorisations) and takes max_stance_legs, the
- * largest number of stance (step, leg) pairs of any instance in the batch
- * (<= 21 selects the one-wavefront kernel, <= 42 the two-wavefront one;
- * 0 = assume the worst case 4N).  An instance with more stance pairs than
- * the selected kernel holds gets status QLOCO_BAD_SIZE and NaN forces. */
+ * largest number of stance (step, leg) pairs of any instance in the batch,
+ * or 0 = unknown (assume 4N).  <= 21: one launch of the one-wavefront
+ * kernel; otherwise two launches on the stream, instances with <= 21 stance
+ * pairs in one-wavefront and the others in two-wavefront workgroups.  An
+ * instance with more than 42 stance pairs gets status QLOCO_BAD_SIZE and NaN
+ * forces. */
 int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, const float *x0,
                         const float *x_ref, const float *feet, const uint8_t *contacts,
                         float *u0, float *u, int32_t *status, int32_t *iters,

@@ -37,6 +37,10 @@
 #include "qloco_common.hpp"
 #include "qloco_dpp.inc"
 
+#ifndef QLOCO_W2_GJ_BUCKETS  // second-half chunk buckets in the W = 2 inverse too
+#define QLOCO_W2_GJ_BUCKETS 0
+#endif
+
 namespace qloco {
 
 constexpr int kMaxN = 20;    // max horizon compiled in (BASELINE configs: N <= 20)
@@ -53,6 +57,9 @@ struct SrbdArgs {
   int max_iter, check_termination, scaling, adaptive_rho, rho_interval;
   float rho_tol;
   int warm_start, polish;
+  // instances with nlegs outside [leg_lo, leg_hi] belong to the other
+  // launch of a split batch (qloco_srbd_solve_ex) and are skipped
+  int leg_lo, leg_hi;
   int64_t batch;
   const float *x0, *xref, *feet;
   const uint8_t *contacts;
@@ -337,6 +344,24 @@ __device__ __forceinline__ void gen_p_row(const SrbdLds<W> &S, const PCoef &pc, 
   }
 }
 
+// W = 2: the second half of a row (columns 64..) holds ncol[1] valid
+// columns; its DPP forms run 9 (<= 36 columns), 15 (<= 60) or 16 chunks.
+// The padding columns beyond are identity (zero on valid rows), so the
+// shorter forms are exact.
+__device__ __forceinline__ int half2_chunks(int ncol1) {
+  return ncol1 <= 36 ? 9 : (ncol1 <= 60 ? 15 : 16);
+}
+#define QL_HALF2(C2, NAME36, NAME60, NAME64, ...) \
+  do {                                           \
+    if ((C2) == 9) {                             \
+      NAME36(__VA_ARGS__);                       \
+    } else if ((C2) == 15) {                     \
+      NAME60(__VA_ARGS__);                       \
+    } else {                                     \
+      NAME64(__VA_ARGS__);                       \
+    }                                            \
+  } while (0)
+
 // K_rc <- rs * D_c * P_rc + [sigma I + A' diag(rho) A]_rc, the leg block
 // touching only the lane's own leg columns (static column -> leg map; D_c
 // fanned out from one LDS chunk per lane by DPP).  Returns the diagonal
@@ -344,7 +369,7 @@ __device__ __forceinline__ void gen_p_row(const SrbdLds<W> &S, const PCoef &pc, 
 template <int W>
 __device__ __forceinline__ float finalize_row(const SrbdLds<W> &S, int t, int cbase, float rs,
                                               float add0, float add1, float add2, bool c60,
-                                              Row<W> &K) {
+                                              int c2, Row<W> &K) {
   constexpr int NC = 64 * W;
   const int lane = t & 63;
   const f4v d0 = reinterpret_cast<const f4v *>(S.Dc)[lane & 15];
@@ -355,7 +380,7 @@ __device__ __forceinline__ float finalize_row(const SrbdLds<W> &S, int t, int cb
   }
   if constexpr (W == 2) {
     const f4v d1 = reinterpret_cast<const f4v *>(S.Dc)[16 + (lane & 15)];
-    QL_DPP_MUL64(K.k, 64, d1);
+    QL_HALF2(c2, QL_DPP_MUL36, QL_DPP_MUL60, QL_DPP_MUL64, K.k, 64, d1);
   }
   int cb = cbase, tt = t;
   asm volatile("" : "+v"(cb), "+v"(tt));
@@ -423,7 +448,7 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1>
 // pivot column register is static inside each half), one s_barrier per
 // pivot, the pivot value through LDS.
 template <int H>
-__device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, Row<2> &K) {
+__device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, int c2, Row<2> &K) {
   const int lane = t & 63;
   int nc = __builtin_amdgcn_readfirstlane(nw);
 #pragma unroll
@@ -447,13 +472,23 @@ __device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, Row
     const float g = (tt == k) ? (1.0f - pinv) : v * pinv;
     const float ng = -g;
     QL_DPP_GJ64(K.k, 0, r0, ng);
+#if QLOCO_W2_GJ_BUCKETS
+    QL_HALF2(c2, QL_DPP_GJ36, QL_DPP_GJ60, QL_DPP_GJ64, K.k, 64, r1, ng);  // uniform branch
+#else
+    (void)c2;  // one form: three per pivot triple the (instruction-cache bound) code
     QL_DPP_GJ64(K.k, 64, r1, ng);
+#endif
   }
 }
 
-__device__ __forceinline__ void invert_w2(SrbdLds<2> &S, int t, const int (&ncol)[2], Row<2> &K) {
-  invert_w2_half<0>(S, t, ncol[0], K);
-  invert_w2_half<1>(S, t, ncol[1], K);
+__device__ __forceinline__ void invert_w2(SrbdLds<2> &S, int t, const int (&ncol)[2], int c2,
+                                          Row<2> &K) {
+  invert_w2_half<0>(S, t, ncol[0], c2, K);
+  // the buffer parity restarts with the second half (its first pivot may
+  // reuse the buffer of the first half's last one): all reads of that
+  // buffer must be done before it is rewritten
+  __syncthreads();
+  invert_w2_half<1>(S, t, ncol[1], c2, K);
   __syncthreads();
 }
 
@@ -470,13 +505,16 @@ __device__ unsigned int g_phase[1 << 20];
 #define QL_PHASE(i) ((void)0)
 #endif
 
+#ifndef QLOCO_SRBD_WAVES_PER_EU_W2  // two-wave kernel occupancy
+#define QLOCO_SRBD_WAVES_PER_EU_W2 2
+#endif
 #ifndef QLOCO_SRBD_WAVES_PER_EU  // one-wave kernel occupancy: 3 waves/SIMD = 168 VGPRs, ~no spills
 #define QLOCO_SRBD_WAVES_PER_EU 3
 #endif
 
 template <int W>
 __global__ __launch_bounds__(64 * W)
-__attribute__((amdgpu_waves_per_eu(W == 1 ? QLOCO_SRBD_WAVES_PER_EU : 2)))
+__attribute__((amdgpu_waves_per_eu(W == 1 ? QLOCO_SRBD_WAVES_PER_EU : QLOCO_SRBD_WAVES_PER_EU_W2)))
 void srbd_admm_kernel(const SrbdArgs a) {
   constexpr int NC = 64 * W, NQ = 16 * W;
   __shared__ __attribute__((aligned(16))) SrbdLds<W> S;
@@ -528,6 +566,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
   bsync<W>();
   const int nlegs = uni(S.nlegs);
   const int n = 3 * nlegs;
+  if (nlegs < a.leg_lo || nlegs > a.leg_hi) return;  // the other launch's instance
   if (nlegs > kLegsPerWave * W) {  // uniform: host picks W from the batch max
     if (t < 12) a.u0[b * 12 + t] = NAN;
     if (t == 0 && a.status) a.status[b] = QLOCO_BAD_SIZE;
@@ -542,6 +581,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
   }
   // every valid column below 60: the 60-column DPP forms (uniform)
   const bool c60 = W == 1 && __builtin_amdgcn_readfirstlane(ncol[0]) <= 60;
+  const int c2 = W == 2 ? half2_chunks(__builtin_amdgcn_readfirstlane(ncol[W - 1])) : 16;
   const int lslot = lane / 3;
   const int comp = lane - 3 * lslot;
   const bool valid = (lane < 63) && (kLegsPerWave * wave + lslot < nlegs);
@@ -792,7 +832,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
           }
           if constexpr (W == 2) {
             const f4v d1 = S.bc[buf][16 + (lane & 15)];
-            QL_DPP_ABSMAX64(m0, m1, m2, m3, t0, t1, t2, t3, d1, K.k, 64);
+            QL_HALF2(c2, QL_DPP_ABSMAX36, QL_DPP_ABSMAX60, QL_DPP_ABSMAX64, m0, m1, m2, m3, t0, t1,
+                     t2, t3, d1, K.k, 64);
           }
         }
         // row norm of D P D after this pass (without the running cost scale)
@@ -838,7 +879,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
     {
       float add0, add1, add2;
       leg_block(add0, add1, add2);
-      const float dg = finalize_row<W>(S, t, t - comp, cs * S.Dc[t], add0, add1, add2, c60, K);
+      const float dg = finalize_row<W>(S, t, t - comp, cs * S.Dc[t], add0, add1, add2, c60, c2, K);
       if (first) QL_PHASE(5);
       if constexpr (W == 1) {
         (void)dg;
@@ -853,7 +894,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
         }
       } else {
         (void)dg;
-        invert_w2(S, t, ncol, K);
+        invert_w2(S, t, ncol, c2, K);
       }
       if (first) QL_PHASE(6);
     }
@@ -887,8 +928,10 @@ void srbd_admm_kernel(const SrbdArgs a) {
       const f2v rv = {RV0, rho}, rvi2 = {RVI0, rvi};
       const float m2 = comp == 2 ? 1.0f : 0.0f;
       // C60: n <= 60, columns 60..63 are identity padding (K^-1 entries 0)
-      auto run_block = [&](auto c60_tag) {
+      // W = 2: CH = chunks of the second row half (9 / 15 / 16)
+      auto run_block = [&](auto c60_tag, auto ch_tag) {
       constexpr bool C60 = decltype(c60_tag)::value;
+      constexpr int CH = decltype(ch_tag)::value;
       for (; iter < next; ++iter) {
         // compiler-only barrier: LDS-resident tables (bv, Dc, zb, ...) are
         // re-read where used instead of being hoisted into loop-live registers
@@ -933,7 +976,13 @@ void srbd_admm_kernel(const SrbdArgs a) {
             QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r0, K.k, 0);
             if constexpr (W == 2) {
               const f4v r1 = S.bc[buf][16 + (lane & 15)];
-              QL_DPP_MATVEC64_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
+              if constexpr (CH == 9) {
+                QL_DPP_MATVEC36_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
+              } else if constexpr (CH == 15) {
+                QL_DPP_MATVEC60_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
+              } else {
+                QL_DPP_MATVEC64_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
+              }
             }
             xt = (acc0 + acc1) + (acc2 + acc3);
           }
@@ -953,10 +1002,20 @@ void srbd_admm_kernel(const SrbdArgs a) {
         z = zn;
       }
       };
-      if (c60) {
-        run_block(std::true_type{});
+      if constexpr (W == 1) {
+        if (c60) {
+          run_block(std::true_type{}, std::integral_constant<int, 16>{});
+        } else {
+          run_block(std::false_type{}, std::integral_constant<int, 16>{});
+        }
       } else {
-        run_block(std::false_type{});
+        if (c2 == 9) {
+          run_block(std::false_type{}, std::integral_constant<int, 9>{});
+        } else if (c2 == 15) {
+          run_block(std::false_type{}, std::integral_constant<int, 15>{});
+        } else {
+          run_block(std::false_type{}, std::integral_constant<int, 16>{});
+        }
       }
       const bool can_check = ctm && (iter % ctm == 0);
       const bool do_rho = interval && (iter % interval == 0);
@@ -1165,14 +1224,25 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   a.status = status;
   a.iters = iters;
   a.rho_updates = rho_updates;
-  int legs = max_stance_legs > 0 ? max_stance_legs : 4 * spec->horizon;
+  // W per instance: instances with <= 21 stance legs run one-wave workgroups,
+  // larger ones two-wave workgroups.  When the batch may hold both (the
+  // caller's maximum, or 4N when unknown, exceeds 21) the batch goes through
+  // two launches on the stream, each skipping the other's instances after
+  // counting its stance legs; instances above 42 legs get QLOCO_BAD_SIZE in
+  // the second.
+  const int legs = max_stance_legs > 0 ? max_stance_legs : 4 * spec->horizon;
   hipStream_t st = (hipStream_t)stream;
+  a.leg_lo = 0;
+  a.leg_hi = 1 << 30;
   if (legs <= kLegsPerWave) {
     hipLaunchKernelGGL(srbd_admm_kernel<1>, dim3((unsigned)batch), dim3(64), 0, st, a);
-  } else if (legs <= 2 * kLegsPerWave) {
-    hipLaunchKernelGGL(srbd_admm_kernel<2>, dim3((unsigned)batch), dim3(128), 0, st, a);
   } else {
-    return QLOCO_BAD_SIZE;
+    a.leg_hi = kLegsPerWave;
+    hipLaunchKernelGGL(srbd_admm_kernel<1>, dim3((unsigned)batch), dim3(64), 0, st, a);
+    QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel<1> launch");
+    a.leg_lo = kLegsPerWave + 1;
+    a.leg_hi = 1 << 30;
+    hipLaunchKernelGGL(srbd_admm_kernel<2>, dim3((unsigned)batch), dim3(128), 0, st, a);
   }
   QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel launch");
   return QLOCO_OK;

@@ -23,12 +23,12 @@ def dpp(dst, src, other, j):
         dst, src, other, j)
 
 
-def matvec(acc):
+def matvec(acc, nch=16):
     # outputs A0..A3 = %0..%3, inputs R.x..R.w = %4..%7, KK[B+c] = %8+c.  Without
     # acc the first group is a v_mul (no accumulator zeroing).  R comes straight
     # from a ds_read (no VALU write); s_nop 1 covers a compiler-inserted copy.
     body = ["s_nop 1"]
-    for j in range(16):
+    for j in range(nch):
         for e in range(4):
             if j == 0 and not acc:
                 body.append("v_mul_f32_dpp %%%d, %%%d, %%%d row_newbcast:0 row_mask:0xf bank_mask:0xf"
@@ -37,8 +37,8 @@ def matvec(acc):
                 body.append(dpp(e, 4 + e, 8 + 4 * j + e, j))
     outs = ", ".join(('"+v"(A%d)' if acc else '"=&v"(A%d)') % e for e in range(4))
     ins = ", ".join(['"v"((R).x)', '"v"((R).y)', '"v"((R).z)', '"v"((R).w)'] +
-                    ['"v"((KK)[(B) + %d])' % c for c in range(64)])
-    name = "QL_DPP_MATVEC64_ACC" if acc else "QL_DPP_MATVEC64"
+                    ['"v"((KK)[(B) + %d])' % c for c in range(4 * nch)])
+    name = ("QL_DPP_MATVEC%d_ACC" if acc else "QL_DPP_MATVEC%d") % (4 * nch)
     what = "+=" if acc else "="
     return ("// A_e %s sum_j KK[B + 4j + e] * R_e(lane j of the row)\n" % what +
             "#define " + name + "(A0, A1, A2, A3, R, KK, B) \\\n  asm(\"" +
@@ -115,5 +115,8 @@ if __name__ == "__main__":
                 absmax() + "\n" + matvec2() + "\n" +
                 # 60-column forms: n <= 60 (every N = 10 trot / pace instance) --
                 # columns 60..63 are identity padding, their updates are zero
-                gj(15) + "\n" + mul(15) + "\n" + absmax(15) + "\n" + matvec2(15))
+                gj(15) + "\n" + mul(15) + "\n" + absmax(15) + "\n" + matvec2(15) + "\n" +
+                # W = 2 second-half forms (columns 64.. of the row): 60 and 36 columns
+                matvec(True, 15) + "\n" + matvec(True, 9) + "\n" + gj(9) + "\n" + mul(9) + "\n" +
+                absmax(9))
     print(OUT)
