@@ -149,10 +149,28 @@ __device__ __forceinline__ float wsum(float v) {
 }
 
 // Block-wide reductions (wave-uniform results).
+// Wave max of a NON-NEGATIVE float: the bits order like unsigned integers,
+// so v_max_u32_dpp does each step in one op (no NaN canonicalisation): the
+// four in-row steps, then row_bcast:15 / row_bcast:31 fold the rows into lane
+// 63 (gfx9 DPP), read once.
+#define QL_DMAXU(U, CTRL)                                                       \
+  asm("s_nop 1\n\tv_max_u32_dpp %0, %0, %0 " CTRL " bank_mask:0xf" : "+v"(U))
+__device__ __forceinline__ float wmax_nonneg(float v) {
+  unsigned u = __builtin_bit_cast(unsigned, v);
+  QL_DMAXU(u, "quad_perm:[1,0,3,2] row_mask:0xf");
+  QL_DMAXU(u, "quad_perm:[2,3,0,1] row_mask:0xf");
+  QL_DMAXU(u, "row_ror:4 row_mask:0xf");
+  QL_DMAXU(u, "row_ror:8 row_mask:0xf");
+  QL_DMAXU(u, "row_bcast:15 row_mask:0xa");  // rows 1, 3 += rows 0, 2
+  QL_DMAXU(u, "row_bcast:31 row_mask:0xc");  // rows 2, 3 += lane 31
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(u, 63));
+}
+
+// Block-wide max of NON-NEGATIVE values (residual norms, |q|).
 template <int W, int NV>
 __device__ __forceinline__ void bmax(float (&v)[NV], float (*red)[16]) {
 #pragma unroll
-  for (int k = 0; k < NV; ++k) v[k] = wmax(v[k]);
+  for (int k = 0; k < NV; ++k) v[k] = wmax_nonneg(v[k]);
   if constexpr (W > 1) {
     const int wave = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0)
@@ -206,6 +224,9 @@ __device__ __forceinline__ float bqp_t(const SrbdLds<W> &S, int step, int comp, 
 template <int W>
 __device__ __forceinline__ void row_scans(SrbdLds<W> &S, int N, bool forward) {
   const int r = threadIdx.x;
+#ifdef QLOCO_ABLATE_NO_SCAN  // timing experiments only
+  if (forward) return;
+#endif
   if (r >= 12) return;
   const bool brow = r >= 6;
   float v[kMaxN];
@@ -235,11 +256,55 @@ __device__ __forceinline__ void row_scans(SrbdLds<W> &S, int N, bool forward) {
   }
 }
 
+// P x phase (b) in one pass: the prefix scan over steps, Q and the weighted
+// suffix scan compose to W[j][r] = q2[r] sum_k Kx(j,k) agg_k[r] with Kx = K0
+// on b rows and K2 on e rows -- the horizon sums of the k0k2 table
+// (sum_{i >= max(j,k)} 1 and sum_{i >= max(j,k)} (i-j)(i-k)).  All lanes, 12N
+// outputs, the table row and the aggregates read up front when NB (= N) is
+// a compile-time constant (N = 10); other horizons use rolled loops.
+template <int W, int NB>
+__device__ __forceinline__ void horizon_rows(SrbdLds<W> &S, int N) {
+  constexpr int NT = 64 * W;
+  if constexpr (NB == 0) {  // any horizon: rolled loops (cold configurations)
+    for (int idx = threadIdx.x; idx < 12 * N; idx += NT) {
+      const int j = idx / 12, r = idx - 12 * j;
+      const f2v *kr = &S.k0k2[j * (kMaxN + 1)];
+      float acc = 0.0f;
+      for (int k = 0; k < N; ++k) acc = fmaf(r >= 6 ? kr[k].x : kr[k].y, S.err[12 * k + r], acc);
+      S.Wc[idx] = S.q2[r] * acc;
+    }
+    return;
+  }
+#pragma unroll
+  for (int pass = 0; pass < (12 * (NB > 0 ? NB : 1) + NT - 1) / NT; ++pass) {
+    const int idx = threadIdx.x + NT * pass;
+    if (idx < 12 * N) {
+      const int j = idx / 12, r = idx - 12 * j;
+      const f2v *kr = &S.k0k2[j * (kMaxN + 1)];
+      float a0 = 0.0f, a1 = 0.0f;
+      if (r >= 6) {
+#pragma unroll
+        for (int k = 0; k < NB; k += 2) {
+          a0 = fmaf(kr[k].x, S.err[12 * k + r], a0);
+          if (k + 1 < NB) a1 = fmaf(kr[k + 1].x, S.err[12 * (k + 1) + r], a1);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < NB; k += 2) {
+          a0 = fmaf(kr[k].y, S.err[12 * k + r], a0);
+          if (k + 1 < NB) a1 = fmaf(kr[k + 1].y, S.err[12 * (k + 1) + r], a1);
+        }
+      }
+      S.Wc[idx] = S.q2[r] * (a0 + a1);
+    }
+  }
+}
+
 // Unscaled (P x)_v, P = Bqp' Q Bqp + R.  Caller has written S.xs (unscaled
 // x, 0 on padding) and synced.  Three phases, all lanes busy:
 //  (a) per-step aggregates agg_j[s] = sum_{v in step j} Bcoef(v, s) x_v
 //  (b) state rows s_i (b rows: prefix sum, e rows: weighted prefix sum),
-//      w_i = Q s_i, suffix weights W0 / W1 per (j, r) -> S.Wc (row_scans)
+//      w_i = Q s_i, suffix weights W0 / W1 per (j, r) -> S.Wc (horizon_rows)
 //  (c) this lane's (Bqp' w)_v + R x_v
 template <int W>
 __device__ __forceinline__ float p_times_x(SrbdLds<W> &S, int N, bool valid, int step, int comp,
@@ -255,20 +320,32 @@ __device__ __forceinline__ float p_times_x(SrbdLds<W> &S, int N, bool valid, int
     float acc = 0.0f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      // loads from a valid pair on every lane (pair 0 when past the step's
+      // last), the term masked: the 24 LDS reads issue together instead of
+      // one divergent round trip per pair
       const int p = p0 + q;
-      if (p < p1) {
-        const int vb = 64 * (p / kLegsPerWave) + 3 * (p % kLegsPerWave);
-        const float *bf = reinterpret_cast<const float *>(&S.bv[vb][0]);
-        const float xa = S.xs[vb], xb = S.xs[vb + 1], xc = S.xs[vb + 2];
-        const float ev = bf[off] * xa + bf[8 + off] * xb + bf[16 + off] * xc;
-        const float xsel = sc == 0 ? xa : (sc == 1 ? xb : xc);
-        acc += (sg & 1) ? dsc * xsel : ev;
-      }
+      const bool ok = p < p1;
+      const int pc = ok ? p : 0;
+      const int vb = 64 * (pc / kLegsPerWave) + 3 * (pc % kLegsPerWave);
+      const float *bf = reinterpret_cast<const float *>(&S.bv[vb][0]);
+      const float xa = S.xs[vb], xb = S.xs[vb + 1], xc = S.xs[vb + 2];
+      const float ev = bf[off] * xa + bf[8 + off] * xb + bf[16 + off] * xc;
+      const float xsel = sc == 0 ? xa : (sc == 1 ? xb : xc);
+      const float term = (sg & 1) ? dsc * xsel : ev;
+      acc += ok ? term : 0.0f;
     }
     S.err[idx] = acc;
   }
   bsync<W>();
+#ifndef QLOCO_PX_SCANS
+  if (N == 10) {
+    horizon_rows<W, 10>(S, N);
+  } else {
+    horizon_rows<W, 0>(S, N);
+  }
+#else
   row_scans<W>(S, N, true);
+#endif
   bsync<W>();
   return valid ? bqp_t<W>(S, step, comp, lo, hi, dtm, dt2m) + r2v * xu : 0.0f;
 }
@@ -675,6 +752,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
     }
     S.err[idx] = S.q2[s] * (xf - a.xref[b * 13 * N + 13 * i + s]);
   }
+  // rows past the horizon stay zero for good (horizon_rows reads them)
+  for (int idx = 12 * N + t; idx < 12 * kMaxN; idx += NC) S.err[idx] = 0.0f;
   bsync<W>();
   row_scans<W>(S, N, false);
   bsync<W>();
@@ -744,8 +823,12 @@ void srbd_admm_kernel(const SrbdArgs a) {
     S.xs[t] = valid ? x * Drl : 0.0f;
     bsync<W>();
     const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
+#ifdef QLOCO_ABLATE_NO_PX  // timing experiments only
+    const float pxo = x * Drl;
+#else
     const float pxo = p_times_x<W>(S, N, valid, (int)bhi.z, comp, blo, bhi, S.aux[0][t], x * Drl,
                                    dtm, dt2m);
+#endif
     const float Dinv = __builtin_amdgcn_rcpf(Drl);
     const f2v Einv = {__builtin_amdgcn_rcpf(S.aux[1][t]), __builtin_amdgcn_rcpf(S.aux[2][t])};
     const f4v arz = S.arz[t];
