@@ -69,6 +69,16 @@ def srbd_flops_executed(n, iters, rho_updates, horizon, checks):
     return build + fac + iters + chk
 
 
+def _config_tag(N, gait, B):
+    """Which BASELINE.json config a bench line measures (per-GPU share for the
+    8-GPU configs: 524288/8 = 65536, 1048576/8 = 131072)."""
+    tags = {(10, "trot", 4096): " (BASELINE configs[1])",
+            (16, "trot", 65536): " (BASELINE configs[2])",
+            (20, "pace", 65536): " (BASELINE configs[3], 1/8 share)",
+            (10, "mixed", 131072): " (BASELINE configs[4], 1/8 share)"}
+    return tags.get((N, gait, B), "")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -177,8 +187,8 @@ def main():
         "dtype": "f32",
         "data": "synthetic (counter-based generator, seed %d, DESIGN.md §4)" % SEED,
         "config": {
-            "workload": "Go1 %s convex MPC N=%d fp32, batch=%d per GPU (BASELINE configs[1])"
-                        % (args.gait, N, B),
+            "workload": "Go1 %s convex MPC N=%d fp32, batch=%d per GPU%s"
+                        % (args.gait, N, B, _config_tag(N, args.gait, B)),
             "horizon": N, "batch_per_gpu": B, "gait": args.gait,
             "solver": "OSQP-algorithm ADMM, default settings (eps 1e-3, adaptive rho)",
             "parallelism": "dp%d (instance shards, RCCL all-gather of u0)" % world,
