@@ -137,6 +137,26 @@ int qo_body_theta_mpc(qo_body_state *s, int i, const double bodyangle_state[4],
                       double com_traj[14], int *eqp_status);
 
 /* ------------------------------------------------------------------ */
+/* rt_mpc_qp node tick: gait_fast.cpp:505-735 + PRMPCClass reference     */
+/* generators (rt_tick.c).  One opaque record per robot.                */
+/* ------------------------------------------------------------------ */
+#define QO_RT_SCHED 8
+typedef struct qo_rt qo_rt;
+/* PRMPCClass() + Initialize() + gait_fast.cpp main() init, n robots */
+qo_rt *qo_rt_create_n(int64_t n);
+void qo_rt_destroy_n(qo_rt *arr, int64_t n);
+/* One loop iteration per robot with the latest /MPC/Gait gait[n*100] and
+ * /control2rtmpc/state ctrl[n*25] -> /rtMPC/traj traj[n*100] and the last
+ * /rt2nrt/state nrt[n*25].  Optional: gen[n*60] = foorpr_gen | foortheta_gen,
+ * sched[n*QO_RT_SCHED] = bjx1, bjxx, t_end_footstep, count_in_rt_mpc, t_int,
+ * body EiQuadProg status (-1: body_theta_mpc not called), flags (bit 0:
+ * /rt2nrt/state published), bjx2. */
+void qo_rt_tick_n(qo_rt *arr, int64_t n, const double *gait, const double *ctrl, double *traj,
+                  double *nrt, double *gen, int32_t *sched);
+/* row-major 4x4 inverse used for solve_AAA_inv* (Gauss-Jordan, partial pivoting) */
+void qo_inv4(const double A[16], double Ainv[16]);
+
+/* ------------------------------------------------------------------ */
 /* SRBD convex MPC: ConvexMpc + A1RobotControl::compute_grf            */
 /* ------------------------------------------------------------------ */
 #define QO_NX 13
