@@ -238,6 +238,46 @@ int qloco_leg_ik(int64_t n, const double *pos_des, const double *q_ini, const in
                  const double *body_p, const double *body_r, double *q_out, double *pos,
                  double *jac, int32_t *updates, void *stream);
 
+/* ====================================================================== */
+/* 6. rt_mpc_qp node tick, batched                 */
+/*    replaces one iteration of the rt node loop, unitree_ros/rt_mpc_qp/   */
+/*    src/gait_fast.cpp:505-735: callbacks (:79-110), counters and         */
+/*    /rt2nrt/state (:512-527), xget_position_interpolation (:113-372 ->   */
+/*    PRMPCClass::XGetSolution_position_mod3, PRMPCClass.cpp:1170-1261),   */
+/*    Foot_trajectory_solve_mod2 (:1756-2195) + Indexfind (:716-738),      */
+/*    XGetSolution_Foot_rotation (:2255-2380), body_theta_mpc (:379-714)   */
+/*    and the /rtMPC/traj message (gait_fast.cpp:633-729)                  */
+/* ====================================================================== */
+/* Wire formats, one message per robot, row-major [B][len], double:
+ *   /MPC/Gait            gait_msg[B*100]  (NLPRTControlClass.cpp:284-392;
+ *                        [86..94] = Nrtfoorpr_gen, [99] = mpc_gait_flag)
+ *   /control2rtmpc/state ctrl_msg[B*25]   ([0] > 0 starts the loop; [10],
+ *                        [11], [13], [14] = bodyangle_state, gait_fast.cpp:105-108)
+ *   /rtMPC/traj          traj_msg[B*100]  ([0..35] = gait_msg[0..35],
+ *                        [36..86] = low_mpc_gait_inte, [86] = 0 (the node's
+ *                        wall-clock duration), [98] = (int)_tx_total/0.001,
+ *                        [99] = count_in_rt_loop)
+ *   /rt2nrt/state        nrt_msg[B*25]    (last published state_to_MPC)  */
+#define QLOCO_GAIT_MSG_LEN 100
+#define QLOCO_CTRL_MSG_LEN 25
+#define QLOCO_TRAJ_MSG_LEN 100
+#define QLOCO_NRT_MSG_LEN 25
+/* sched[B*8] (optional): bjx1, bjxx, t_end_footstep, count_in_rt_mpc, t_int,
+ * body EiQuadProg status (-1 = body_theta_mpc not called this tick),
+ * /rt2nrt/state published this tick (0/1), bjx2 */
+#define QLOCO_RT_SCHED_LEN 8
+/* Bytes of the device workspace holding B robots' node + PRMPCClass state. */
+int64_t qloco_rt_workspace_bytes(int64_t batch);
+/* PRMPCClass() + Initialize() + gait_fast.cpp main() init (:384-502) for B
+ * robots, on device. */
+int qloco_rt_init(int64_t batch, void *workspace, void *stream);
+/* One loop iteration for B robots, given each robot's latest /MPC/Gait and
+ * /control2rtmpc/state (device pointers).  gen[B*60] (optional) =
+ * foorpr_gen (30) | foortheta_gen (30). */
+int qloco_rt_tick(int64_t batch, void *workspace, const double *gait_msg,
+                  const double *ctrl_msg, double *traj_msg, double *nrt_msg, double *gen,
+                  int32_t *sched, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,19 @@ struct qo_rt {
 static const double DT_SLOW = 0.025, DT_FAST = 0.01, TSTEP = 0.7; /* gait:: :8-9,26 */
 static const double HALF_HIP = 0.12675;                            /* :19 */
 
+/* std::pow(t, 3) / pow(t, 2) of the reference (PRMPCClass.cpp:1199-1211,
+ * :1901-1906, :2227-2230) as a compensated cube (error-free products via
+ * fma, one final rounding) and an exact-rounded square: glibc's pow is only
+ * <1 ulp, which the ill-conditioned cubic fits (solve_AAA_inv2 near the
+ * swing's knot crossings) amplify, so every restatement (this file, the
+ * GPU kernel, tests/rt_ref.py) uses these same primitives. */
+static double sq(double x) { return x * x; }
+static double cube(double x) {
+  const double p = x * x, e = fma(x, x, -p);
+  const double hi = p * x, lo = fma(p, x, -hi);
+  return hi + (lo + e * x);
+}
+
 /* Dense 4x4 inverse, Gauss-Jordan with partial pivoting (Eigen's
  * Matrix4d::inverse() restated; agreement to rounding, not bit-exact).
  * A, Ainv row-major. */
@@ -102,9 +115,9 @@ static void aaa_inv_mod(double out_colmajor[16]) {
   const double t[4] = {-DT_SLOW, 0, DT_SLOW, 2 * DT_SLOW};
   double A[16], Ai[16];
   for (int r = 0; r < 4; ++r) {
-    A[r * 4 + 0] = pow(t[r], 3);
-    A[r * 4 + 1] = pow(t[r], 2);
-    A[r * 4 + 2] = pow(t[r], 1);
+    A[r * 4 + 0] = cube(t[r]);
+    A[r * 4 + 1] = sq(t[r]);
+    A[r * 4 + 2] = (t[r]);
     A[r * 4 + 3] = 1;
   }
   qo_inv4(A, Ai);
@@ -114,10 +127,10 @@ static void aaa_inv_mod(double out_colmajor[16]) {
 
 /* solve_AAA_inv2, :2225-2237; returns row-major */
 static void aaa_inv2(const double tp[3], double Ai[16]) {
-  double A[16] = {pow(tp[0], 3), pow(tp[0], 2), pow(tp[0], 1), 1,
-                  pow(tp[1], 3), pow(tp[1], 2), pow(tp[1], 1), 1,
-                  pow(tp[2], 3), pow(tp[2], 2), pow(tp[2], 1), 1,
-                  3 * pow(tp[2], 2), 2 * pow(tp[2], 1), pow(tp[2], 0), 0};
+  double A[16] = {cube(tp[0]), sq(tp[0]), (tp[0]), 1,
+                  cube(tp[1]), sq(tp[1]), (tp[1]), 1,
+                  cube(tp[2]), sq(tp[2]), (tp[2]), 1,
+                  3 * sq(tp[2]), 2 * (tp[2]), 1.0, 0};
   qo_inv4(A, Ai);
 }
 
@@ -204,9 +217,9 @@ static void position_mod3(const qo_rt *s, int walktime, double dt_sample, const 
   if (walktime > s->t_end_footstep) return;
   for (int jx = 0; jx < NH; jx++) {
     double t_cur = (walktime * dt_sample + jx * dt_sample);
-    double tp[4] = {pow(t_cur, 3), pow(t_cur, 2), pow(t_cur, 1), pow(t_cur, 0)};
-    double tv[4] = {3 * pow(t_cur, 2), 2 * pow(t_cur, 1), 1, 0};
-    double ta[4] = {6 * pow(t_cur, 1), 2, 0, 0};
+    double tp[4] = {cube(t_cur), sq(t_cur), (t_cur), 1.0};
+    double tv[4] = {3 * sq(t_cur), 2 * (t_cur), 1, 0};
+    double ta[4] = {6 * (t_cur), 2, 0, 0};
     /* row vectors times _AAA_inv_mod (left to right), then times temp */
     double rp[4], rv[4], ra[4];
     for (int c = 0; c < 4; ++c) {
@@ -315,9 +328,9 @@ static void swing_axis(qo_rt *s, const double Ai[16], double t_des, int p, int v
     for (int c = 0; c < 4; ++c) acc += Ai[r * 4 + c] * plan[c];
     co[r] = acc;
   }
-  double tp[4] = {pow(t_des, 3), pow(t_des, 2), pow(t_des, 1), 1};
-  double tv[4] = {3 * pow(t_des, 2), 2 * pow(t_des, 1), 1, 0};
-  double ta[4] = {6 * pow(t_des, 1), 2, 0, 0};
+  double tp[4] = {cube(t_des), sq(t_des), (t_des), 1};
+  double tv[4] = {3 * sq(t_des), 2 * (t_des), 1, 0};
+  double ta[4] = {6 * (t_des), 2, 0, 0};
   double xp = 0, xv = 0, xa = 0;
   for (int c = 0; c < 4; ++c) {
     xp += tp[c] * co[c];
@@ -360,6 +373,10 @@ static void foot_traj_mod2(qo_rt *s, int j_indexx, int stopwalking, const double
     s->fxyz[1][0] = -s->stepwidth0;                       /* :1814 */
     if ((*bjx1 >= 2) && (j_index <= s->t_end_footstep)) {
       const int b1 = *bjx1, bx = s->bjxx;
+      /* _bjxx-2 < 0 is reachable only with a step period under 0.1 s (the DSP
+       * window td = 0.1 ts shorter than one tick); the reference then reads
+       * out of bounds -- defined here as index 0 */
+      const int bm = bx >= 2 ? bx - 2 : 0;
       /* support leg holds (:1866-1876 / :2003-2008); swing leg = other */
       const int sx = (b1 % 2 == 0) ? LX : RX; /* support */
       const int wx = (b1 % 2 == 0) ? RX : LX; /* swing   */
@@ -388,13 +405,13 @@ static void foot_traj_mod2(qo_rt *s, int j_indexx, int stopwalking, const double
           double Ai[16];
           aaa_inv2(tp, Ai);
           swing_axis(s, Ai, t_des, wx + 0, wx + 3, wx + 6, k,
-                     (s->fxyz[0][bx - 2] + s->fxyz[0][bx]) / 2, s->fxyz[0][bx]);
+                     (s->fxyz[0][bm] + s->fxyz[0][bx]) / 2, s->fxyz[0][bx]);
           if ((j_index + 1 - rt) * DT_FAST < s->td[b1 - 1] + DT_FAST)
-            s->ry_left_right = (s->fxyz[1][bx] + s->fxyz[1][bx - 2]) / 2;
+            s->ry_left_right = (s->fxyz[1][bx] + s->fxyz[1][bm]) / 2;
           swing_axis(s, Ai, t_des, wx + 1, wx + 4, wx + 7, k, s->ry_left_right, s->fxyz[1][bx]);
           /* std::max(a, b) returns a unless a < b */
-          const double zmax = (s->fxyz[2][bx - 2] < s->fxyz[2][bx]) ? s->fxyz[2][bx]
-                                                                   : s->fxyz[2][bx - 2];
+          const double zmax = (s->fxyz[2][bm] < s->fxyz[2][bx]) ? s->fxyz[2][bx]
+                                                                   : s->fxyz[2][bm];
           swing_axis(s, Ai, t_des, wx + 2, wx + 5, wx + 8, k, zmax + s->lift[b1 - 1],
                      s->fxyz[2][bx]);
           for (int ax = 0; ax < 3; ++ax)

@@ -65,6 +65,9 @@ SIGNATURES = {
     "qloco_body_state_init_host": (C.c_int, [i64, vp]),
     "qloco_body_mpc_step": (C.c_int, [i64] + [vp] * 10),
     "qloco_body_indexfind": (C.c_int, [i64, vp, vp, vp]),
+    "qloco_rt_workspace_bytes": (C.c_int64, [i64]),
+    "qloco_rt_init": (C.c_int, [i64, vp, vp]),
+    "qloco_rt_tick": (C.c_int, [i64, vp, vp, vp, vp, vp, vp, vp, vp]),
 }
 
 

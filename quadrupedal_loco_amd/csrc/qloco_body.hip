@@ -124,6 +124,13 @@ struct BodyArgs {
   const double *bodyangle_state, *zmp_ref, *angle_ref, *rfoot_ref, *lfoot_ref, *comacc_ref;
   double *state, *com_traj;
   int *status;
+  // rt node tick (qloco_rt.hip): the robot's own _tx (Foot_trajectory_solve_mod2
+  // rewrites it, PRMPCClass.cpp:1773-1779) at tx[j * tx_stride + inst], and a
+  // mask of the robots whose loop calls body_theta_mpc this tick.  NULL: the
+  // Initialize() schedule for every instance / all run.
+  const double *tx;
+  int64_t tx_stride;
+  const int32_t *run;
 };
 
 struct BodyLds {
@@ -138,6 +145,12 @@ struct BodyLds {
 __device__ __forceinline__ int indexfind(const BodyConsts &k, double goal) {
   int j = 0;
   while (j < BSTEPS && goal >= k.tx[j]) j++;
+  return j - 1;
+}
+// ... on a per-robot schedule (strided)
+__device__ __forceinline__ int indexfind(const double *tx, int64_t stride, double goal) {
+  int j = 0;
+  while (j < BSTEPS && goal >= tx[j * stride]) j++;
   return j - 1;
 }
 
@@ -180,14 +193,20 @@ __global__ __launch_bounds__(64) void body_mpc_kernel(const BodyArgs a) {
   bool active = false;
   const int off = (int)round(1.0 / K.dt_mpc);  // height_offset_time / dt (:395)
   int bjx1 = (int)st[26], bjx2 = (int)st[27], t_yu = (int)st[28];
-  if (i >= off) {
+  const bool run = a.run ? a.run[inst] != 0 : true;
+  if (run && i >= off) {
     i -= off;
     active = i < (K.nsum_mpc - BNH);  // :403
   }
   if (active) {
     const double t_f0 = (i + 1) * K.dt_mpc, t_f3 = (i + BNH) * K.dt_mpc;  // :406
-    bjx1 = indexfind(K, t_f0) + 1;
-    bjx2 = indexfind(K, t_f3) + 1;
+    if (a.tx) {
+      bjx1 = indexfind(a.tx + inst, a.tx_stride, t_f0) + 1;
+      bjx2 = indexfind(a.tx + inst, a.tx_stride, t_f3) + 1;
+    } else {
+      bjx1 = indexfind(K, t_f0) + 1;
+      bjx2 = indexfind(K, t_f3) + 1;
+    }
     t_yu = (i + 1) % K.nstepx;
     double copx[BNH], copy[BNH];
     const double *sup = lfoot_ref, *oth = rfoot_ref;  // CoP reference, :427-499
@@ -341,6 +360,12 @@ __global__ __launch_bounds__(64) void body_mpc_kernel(const BodyArgs a) {
   if (li == 0 && a.status) a.status[inst] = active ? status : QLOCO_OK;
 }
 
+int body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyangle_state,
+                    const double *zmp_ref, const double *angle_ref, const double *rfoot_ref,
+                    const double *lfoot_ref, const double *comacc_ref, double *state,
+                    double *com_traj, int32_t *status, const double *tx, int64_t tx_stride,
+                    const int32_t *run, hipStream_t stream);
+
 __global__ void indexfind_kernel(const BodyConsts k, int64_t batch, const double *t, int *j) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < batch) j[idx] = indexfind(k, t[idx]);
@@ -368,6 +393,17 @@ extern "C" int qloco_body_mpc_step(int64_t batch, const int32_t *i,
   if (!i || !bodyangle_state || !zmp_ref || !angle_ref || !rfoot_ref || !lfoot_ref ||
       !comacc_ref || !state || !com_traj)
     return QLOCO_ERR_ARG;
+  return body_mpc_launch(batch, i, bodyangle_state, zmp_ref, angle_ref, rfoot_ref, lfoot_ref,
+                         comacc_ref, state, com_traj, status, nullptr, 0, nullptr,
+                         (hipStream_t)stream);
+}
+
+int qloco::body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyangle_state,
+                           const double *zmp_ref, const double *angle_ref,
+                           const double *rfoot_ref, const double *lfoot_ref,
+                           const double *comacc_ref, double *state, double *com_traj,
+                           int32_t *status, const double *tx, int64_t tx_stride,
+                           const int32_t *run, hipStream_t stream) {
   BodyArgs a;
   memset(&a, 0, sizeof(a));
   body_constants(a.k);
@@ -382,8 +418,11 @@ extern "C" int qloco_body_mpc_step(int64_t batch, const int32_t *i,
   a.state = state;
   a.com_traj = com_traj;
   a.status = status;
+  a.tx = tx;
+  a.tx_stride = tx_stride;
+  a.run = run;
   const unsigned blocks = (unsigned)((batch + GI_GROUPS - 1) / GI_GROUPS);
-  hipLaunchKernelGGL(body_mpc_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(body_mpc_kernel, dim3(blocks), dim3(64), 0, stream, a);
   QLOCO_HIP_CHECK(hipGetLastError(), "body_mpc_kernel launch");
   return QLOCO_OK;
 }

@@ -1,0 +1,704 @@
+// qloco_rt.hip -- batched rt_mpc_qp node tick (gfx950), SURVEY.md §8f rows 2-3.
+//
+// One tick = one iteration of the rt node's 100 Hz loop for B robots
+// (unitree_ros/rt_mpc_qp/src/gait_fast.cpp:505-735): the subscriber
+// callbacks on the latest /MPC/Gait and /control2rtmpc/state messages
+// (:79-110), the loop counters and /rt2nrt/state (:512-527), the cubic
+// interpolation of the slow-MPC references (xget_position_interpolation,
+// :113-372 -> PRMPCClass::XGetSolution_position_mod3, PRMPCClass.cpp:
+// 1170-1261), the contact schedule and swing-foot generator
+// (Foot_trajectory_solve_mod2, :1756-2195, with Indexfind :716-738), the
+// foot rotation generator (XGetSolution_Foot_rotation, :2255-2380), the
+// body-MPC reference packing (:557-616), body_theta_mpc (qloco_body.hip)
+// and the /rtMPC/traj message (:633-729).
+//
+// Three launches on one stream:
+//   rt_pre_kernel    one robot per lane: everything before body_theta_mpc;
+//                    writes the body kernel's reference arrays and run mask
+//   body_mpc_kernel  4 robots per wave (16-lane Goldfarb-Idnani groups), on
+//                    each robot's own _tx schedule
+//   rt_post_kernel   one robot per lane: packs /rtMPC/traj, /rt2nrt/state
+//
+// State lives in one device workspace: the node/generator members
+// field-major (SoA: field f of robot r at d[f*B + r], so every lane access of
+// a field is one coalesced 512-byte row per wave), the body-MPC records
+// (QLOCO_BODY_STATE_LEN doubles per robot, shared with qloco_body_mpc_step)
+// and per-tick scratch.  fp64 throughout, compiled without FMA contraction
+// so the schedule arithmetic follows the restatement (oracle/rt_tick.c)
+// operation for operation; schedule integers are bit-exact.
+//
+// Reference quirks kept (see oracle/rt_tick.c): rfoot_mpc_ref row 0 holds
+// the y coordinate and row 1 stays 0; t_int += floor(count/2) (int32 wrap);
+// mpc_gait_flag = (int) /MPC/Gait[99]; traj[86] (the node's own wall-clock
+// duration) is 0; stale member values carried between calls.
+#include <math.h>
+#include <string.h>
+
+#include "qloco_common.hpp"
+
+namespace qloco {
+
+int body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyangle_state,
+                    const double *zmp_ref, const double *angle_ref, const double *rfoot_ref,
+                    const double *lfoot_ref, const double *comacc_ref, double *state,
+                    double *com_traj, int32_t *status, const double *tx, int64_t tx_stride,
+                    const int32_t *run, hipStream_t stream);
+
+namespace rt {
+
+constexpr int NS = 27;  // _footstepsnumber
+constexpr int NH = 4;   // _nh
+constexpr double DT_SLOW = 0.025, DT_FAST = 0.01, TSTEP = 0.7, HALF_HIP = 0.12675;
+constexpr double STEPWIDTH0 = 2 * HALF_HIP / 2, TDSP_RATIO = 0.1, FOOTX_MAX = 0.15;
+
+// double fields (SoA offsets, in units of B)
+enum : int {
+  F_TS = 0,
+  F_TD = F_TS + NS,
+  F_LIFT = F_TD + NS,
+  F_TX = F_LIFT + NS,
+  F_FXYZ = F_TX + NS,       // _footxyz_real(a, i) at F_FXYZ + a*NS + i
+  F_TXTOT = F_FXYZ + 3 * NS,
+  F_RYLR = F_TXTOT + 1,
+  F_FOOT = F_RYLR + 1,      // foot array a (RX..LAZ), index k (0..5) at F_FOOT + a*6 + k
+  F_RFR = F_FOOT + 18 * 6,  // _Rfoot_r (3x5 col-major)
+  F_LFR = F_RFR + 15,
+  F_COM = F_LFR + 15,       // COM_in1, COM_in2, COMxyz_ref, COM_ref2, COMv_ref
+  F_ACC = F_COM + 15,       // COMacc_in1, _in2, _ref, _ref2
+  F_ZMP = F_ACC + 12,       // zmp_in1, _in2, zmpxyz_ref, zmp_ref2
+  F_DCM = F_ZMP + 12,       // dcm_in1, _in2, dcmxyz_ref, dcm_ref2
+  F_RPY = F_DCM + 12,       // rpy_mpc_body (21)
+  F_CACC = F_RPY + 21,      // comacc_inter
+  F_ZINT = F_CACC + 21,     // zmp_inter
+  F_DINT = F_ZINT + 21,     // dcm_inter
+  F_FOORPR = F_DINT + 21,   // foorpr_gen (30)
+  F_FTHETA = F_FOORPR + 30, // foortheta_gen (30)
+  F_BTHX = F_FTHETA + 30,   // body_thetax(0..1)
+  F_NRT = F_BTHX + 2,       // state_to_MPC (25)
+  F_DOUBLES = F_NRT + 25
+};
+// int fields
+enum : int { I_LOOP = 0, I_MPC, I_INT, I_TINT, I_FLAGOLD, I_TEND, I_BJXX, I_INTS };
+enum { RX = 0, RY, RZ, RVX, RVY, RVZ, RAX, RAY, RAZ, LX, LY, LZ, LVX, LVY, LVZ, LAX, LAY, LAZ };
+
+struct Ws {  // byte offsets into the workspace
+  int64_t d, n, body, zmp, ang, rft, lft, acc, bas, ct, bi, run, st, total;
+};
+__host__ __device__ inline Ws layout(int64_t B) {
+  Ws w;
+  auto al = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+  w.d = 0;
+  w.n = al(w.d + 8 * F_DOUBLES * B);
+  w.body = al(w.n + 4 * I_INTS * B);
+  w.zmp = al(w.body + 8 * QLOCO_BODY_STATE_LEN * B);
+  w.ang = al(w.zmp + 8 * 10 * B);
+  w.rft = al(w.ang + 8 * 10 * B);
+  w.lft = al(w.rft + 8 * 10 * B);
+  w.acc = al(w.lft + 8 * 10 * B);
+  w.bas = al(w.acc + 8 * 15 * B);
+  w.ct = al(w.bas + 8 * 4 * B);
+  w.bi = al(w.ct + 8 * 14 * B);
+  w.run = al(w.bi + 4 * B);
+  w.st = al(w.run + 4 * B);
+  w.total = al(w.st + 4 * B);
+  return w;
+}
+
+struct RtArgs {
+  int64_t B;
+  char *ws;
+  const double *gait, *ctrl;
+  double *traj, *nrt, *gen;
+  int32_t *sched;
+  double aaa_inv_mod[16];  // solve_AAA_inv_mod1 (:1344-1362), col-major
+};
+
+// per-lane view of one robot's SoA state
+struct Robot {
+  double *d;
+  int32_t *n;
+  int64_t B;
+  __device__ double &D(int f) const { return d[(int64_t)f * B]; }
+  __device__ int32_t &I(int f) const { return n[(int64_t)f * B]; }
+  __device__ double &foot(int a, int k) const { return D(F_FOOT + a * 6 + k); }
+  __device__ double &fxyz(int a, int i) const { return D(F_FXYZ + a * NS + i); }
+};
+
+// Indexfind, xyz = 0 (:716-738), bounded at the 27 steps
+__device__ __forceinline__ int indexfind(const Robot &R, double goal) {
+  int j = 0;
+  while (j < NS && goal >= R.D(F_TX + j)) j++;
+  return j - 1;
+}
+
+// std::pow(t, 3) / pow(t, 2) as in oracle/rt_tick.c: compensated cube (fma
+// error-free products, one final rounding), exact-rounded square
+__host__ __device__ inline double sq(double x) { return x * x; }
+__host__ __device__ inline double cube(double x) {
+  const double p = x * x, e = fma(x, x, -p);
+  const double hi = p * x, lo = fma(p, x, -hi);
+  return hi + (lo + e * x);
+}
+
+// Dense 4x4 inverse, Gauss-Jordan with partial pivoting (row-major), the
+// same algorithm and operation order as oracle/rt_tick.c:qo_inv4
+__host__ __device__ inline void inv4(const double A[16], double Ai[16]) {
+  double M[4][8];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) {
+      M[r][c] = A[r * 4 + c];
+      M[r][4 + c] = (r == c) ? 1.0 : 0.0;
+    }
+  for (int k = 0; k < 4; ++k) {
+    int p = k;
+    for (int r = k + 1; r < 4; ++r)
+      if (fabs(M[r][k]) > fabs(M[p][k])) p = r;
+    if (p != k)
+      for (int c = 0; c < 8; ++c) {
+        const double t = M[k][c];
+        M[k][c] = M[p][c];
+        M[p][c] = t;
+      }
+    const double piv = M[k][k];
+    for (int c = 0; c < 8; ++c) M[k][c] = M[k][c] / piv;
+    for (int r = 0; r < 4; ++r) {
+      if (r == k) continue;
+      const double f = M[r][k];
+      for (int c = 0; c < 8; ++c) M[r][c] = M[r][c] - f * M[k][c];
+    }
+  }
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) Ai[r * 4 + c] = M[r][4 + c];
+}
+
+__device__ void recompute_tx(const Robot &R) {  // :1773-1779
+  for (int i = 0; i < NS; ++i) R.D(F_TD + i) = TDSP_RATIO * R.D(F_TS + i);
+  double t = 0.0;
+  R.D(F_TX) = 0.0;
+  for (int i = 1; i < NS; i++) {
+    t = t + R.D(F_TS + i - 1);
+    t = round(t / DT_SLOW) * DT_SLOW - 0.00001;
+    R.D(F_TX + i) = t;
+  }
+}
+
+// XGetSolution_position_mod3 (:1170-1261): 4 horizon points of the cubic
+// through (in1, in2, ref, ref2) at t = -dt, 0, dt, 2dt (dt = dt_mpc_slow)
+__device__ void position_mod3(const RtArgs &a, const Robot &R, int walktime, int f_in,
+                              int f_out, int t_end) {
+  for (int k = 0; k < 21; ++k) R.D(f_out + k) = 0.0;
+  if (walktime > t_end) return;
+  double in[4][3];
+  for (int q = 0; q < 4; ++q)
+    for (int ax = 0; ax < 3; ++ax) in[q][ax] = R.D(f_in + 3 * q + ax);
+#pragma unroll
+  for (int jx = 0; jx < NH; jx++) {
+    const double t_cur = (walktime * DT_FAST + jx * DT_FAST);
+    const double tp[4] = {cube(t_cur), sq(t_cur), (t_cur), 1.0};
+    const double tv[4] = {3 * sq(t_cur), 2 * (t_cur), 1, 0};
+    const double ta[4] = {6 * (t_cur), 2, 0, 0};
+    double rp[4], rv[4], ra[4];
+    for (int c = 0; c < 4; ++c) {
+      double ap = 0, av = 0, aa = 0;
+      for (int k = 0; k < 4; ++k) {
+        ap += tp[k] * a.aaa_inv_mod[c * 4 + k];
+        av += tv[k] * a.aaa_inv_mod[c * 4 + k];
+        aa += ta[k] * a.aaa_inv_mod[c * 4 + k];
+      }
+      rp[c] = ap;
+      rv[c] = av;
+      ra[c] = aa;
+    }
+    for (int ax = 0; ax < 3; ++ax) {
+      double p = 0, v = 0, acc = 0;
+      for (int k = 0; k < 4; ++k) {
+        p += rp[k] * in[k][ax];
+        v += rv[k] * in[k][ax];
+        acc += ra[k] * in[k][ax];
+      }
+      if (jx == 0) {
+        R.D(f_out + ax) = p;
+        R.D(f_out + 3 + ax) = v;
+        R.D(f_out + 6 + ax) = acc;
+      } else {
+        R.D(f_out + 8 + 3 * jx - 2 + ax) = p;
+      }
+    }
+  }
+}
+
+// one swing-foot axis (:1903-1951 right / :2069-2118 left)
+__device__ __forceinline__ void swing_axis(const Robot &R, const double Ai[16], double t_des,
+                                           int p, int v, int acc, int k, double mid, double end) {
+  const double plan[4] = {R.foot(p, k - 1), mid, end, 0};
+  double co[4];
+  for (int r = 0; r < 4; ++r) {
+    double s = 0;
+    for (int c = 0; c < 4; ++c) s += Ai[r * 4 + c] * plan[c];
+    co[r] = s;
+  }
+  const double tp[4] = {cube(t_des), sq(t_des), (t_des), 1};
+  const double tv[4] = {3 * sq(t_des), 2 * (t_des), 1, 0};
+  const double ta[4] = {6 * (t_des), 2, 0, 0};
+  double xp = 0, xv = 0, xa = 0;
+  for (int c = 0; c < 4; ++c) {
+    xp += tp[c] * co[c];
+    xv += tv[c] * co[c];
+    xa += ta[c] * co[c];
+  }
+  R.foot(p, k) = xp;
+  R.foot(v, k) = xv;
+  R.foot(acc, k) = xa;
+}
+
+// Foot_trajectory_solve_mod2 (PRMPCClass.cpp:1756-2195), _stopwalking = false
+__device__ void foot_traj_mod2(const Robot &R, int j_indexx, const double nrt[9], int &bjx1,
+                               int &bjxx, int &t_end) {
+  const int bjxx_nrt = (int)nrt[0];
+  if (bjxx_nrt >= 0 && bjxx_nrt + 1 < NS) {  // :1758-1764 (unchecked in the reference)
+    R.fxyz(0, bjxx_nrt) = nrt[1];
+    R.fxyz(0, bjxx_nrt + 1) = nrt[2];
+    R.fxyz(1, bjxx_nrt) = nrt[3];
+    R.fxyz(1, bjxx_nrt + 1) = nrt[4];
+    R.fxyz(2, bjxx_nrt) = nrt[5];
+    R.fxyz(2, bjxx_nrt + 1) = nrt[6];
+  }
+  const int bjx_period_nrt = (int)nrt[7];
+  if (nrt[8] > 0 && bjx_period_nrt >= 0 && bjx_period_nrt < NS) R.D(F_TS + bjx_period_nrt) = nrt[8];
+  recompute_tx(R);
+  t_end = (int)round((R.D(F_TX + NS - 1) - 2 * TSTEP) / DT_FAST);  // :1780
+  R.D(F_TXTOT) = R.D(F_TX + NS - 1);
+#pragma unroll
+  for (int kk = 1; kk <= NH; ++kk) {
+    const int j_index = j_indexx + kk - 1, k = kk;
+    if (j_index <= t_end) {  // :1790-1799
+      bjxx = indexfind(R, j_index * DT_FAST) + 1;
+      bjx1 = indexfind(R, (j_index + 1) * DT_FAST) + 1;
+    }
+    if (j_index > t_end)  // :1801-1807
+      for (int i_t = bjx1 + 1; i_t < NS; i_t++) R.D(F_LIFT + i_t) = 0;
+    for (int i_t = 24; i_t < NS; i_t++) R.D(F_LIFT + i_t) = 0;  // :1809-1811
+    R.fxyz(1, 0) = -STEPWIDTH0;                                 // :1814
+    if ((bjx1 >= 2) && (j_index <= t_end)) {
+      const int b1 = bjx1, bx = bjxx;
+      const int bm = bx >= 2 ? bx - 2 : 0;  // reference UB below 0 (oracle/rt_tick.c)
+      const int sx = (b1 % 2 == 0) ? LX : RX;  // support leg holds
+      const int wx = (b1 % 2 == 0) ? RX : LX;  // swing leg
+      for (int ax = 0; ax < 3; ++ax) {
+        const double h = R.foot(sx + ax, k - 1);
+        R.foot(sx + ax, k) = h;
+        R.foot(sx + ax, k + 1) = h;
+      }
+      const double rt = round(R.D(F_TX + b1 - 1) / DT_FAST);
+      const double tdb = R.D(F_TD + b1 - 1), tsb = R.D(F_TS + b1 - 1);
+      if ((j_index + 1 - rt) * DT_FAST < tdb) {  // double support
+        for (int ax = 0; ax < 3; ++ax) {
+          const double h = R.foot(wx + ax, k - 1);
+          R.foot(wx + ax, k) = h;
+          R.foot(wx + ax, k + 1) = h;
+        }
+      } else {
+        const double t_des = (j_index + 1 - rt + 1) * DT_FAST;
+        double tp[3];
+        tp[0] = t_des - DT_FAST;
+        tp[1] = (tdb + tsb) / 2 + 0.0001;
+        tp[2] = tsb - (2 * DT_FAST + 0.001);
+        if (fabs(t_des - tsb) <= (DT_FAST)) {
+          for (int ax = 0; ax < 3; ++ax) {
+            const double e = R.fxyz(ax, bx);
+            R.foot(wx + ax, k) = e;
+            R.foot(wx + ax, k + 1) = e;
+          }
+        } else {
+          const double A[16] = {cube(tp[0]), sq(tp[0]), (tp[0]), 1,
+                                cube(tp[1]), sq(tp[1]), (tp[1]), 1,
+                                cube(tp[2]), sq(tp[2]), (tp[2]), 1,
+                                3 * sq(tp[2]), 2 * (tp[2]), 1.0, 0};
+          double Ai[16];
+          inv4(A, Ai);  // solve_AAA_inv2 (:2225-2237)
+          swing_axis(R, Ai, t_des, wx + 0, wx + 3, wx + 6, k,
+                     (R.fxyz(0, bm) + R.fxyz(0, bx)) / 2, R.fxyz(0, bx));
+          if ((j_index + 1 - rt) * DT_FAST < tdb + DT_FAST)
+            R.D(F_RYLR) = (R.fxyz(1, bx) + R.fxyz(1, bm)) / 2;
+          swing_axis(R, Ai, t_des, wx + 1, wx + 4, wx + 7, k, R.D(F_RYLR), R.fxyz(1, bx));
+          const double z0 = R.fxyz(2, bm), z1 = R.fxyz(2, bx);
+          const double zmax = (z0 < z1) ? z1 : z0;  // std::max
+          swing_axis(R, Ai, t_des, wx + 2, wx + 5, wx + 8, k, zmax + R.D(F_LIFT + b1 - 1), z1);
+          for (int ax = 0; ax < 3; ++ax)
+            R.foot(wx + ax, k + 1) = R.foot(wx + ax, k) + DT_FAST * R.foot(wx + 3 + ax, k);
+        }
+      }
+    } else {
+      if (j_index > t_end) {  // :2152-2160
+        for (int ax = 0; ax < 3; ++ax) {
+          R.foot(RX + ax, k) = R.foot(RX + ax, k - 1);
+          R.foot(LX + ax, k) = R.foot(LX + ax, k - 1);
+        }
+      } else {  // :2163-2166
+        R.foot(RY, k) = -STEPWIDTH0;
+        R.foot(LY, k) = STEPWIDTH0;
+      }
+    }
+  }
+  for (int j = 0; j < 5; j++) {  // :2170-2178
+    R.D(F_FOORPR + 0 + 6 * j) = R.foot(RX, j + 1);
+    R.D(F_FOORPR + 1 + 6 * j) = R.foot(RY, j + 1);
+    R.D(F_FOORPR + 2 + 6 * j) = R.foot(RZ, j + 1);
+    R.D(F_FOORPR + 3 + 6 * j) = R.foot(LX, j + 1);
+    R.D(F_FOORPR + 4 + 6 * j) = R.foot(LY, j + 1);
+    R.D(F_FOORPR + 5 + 6 * j) = R.foot(LZ, j + 1);
+  }
+  for (int f = 0; f < 18; ++f) R.foot(f, 0) = R.foot(f, 1);  // :2180-2197
+}
+
+// XGetSolution_Foot_rotation (PRMPCClass.cpp:2255-2380)
+__device__ void foot_rotation(const Robot &R, int walktimex, int &bjx1, int &bjxx, int t_end) {
+#pragma unroll
+  for (int c = 0; c < NH; ++c) {
+    const int walktime = walktimex + c;
+    if (walktime <= t_end) {
+      bjxx = indexfind(R, walktime * DT_FAST) + 1;
+      bjx1 = indexfind(R, (walktime + 1) * DT_FAST) + 1;
+    }
+    const int b1 = bjx1;
+    if ((b1 >= 2) && (walktime <= t_end)) {
+      const double tsb = R.D(F_TS + b1 - 1), tdb = R.D(F_TD + b1 - 1);
+      const double t_desxx = (walktime + 1) * DT_FAST - (R.D(F_TX + b1 - 1) + 2 * tdb / 4);
+      const double ph = t_desxx + 2 * tdb / 4;
+      const double dx = R.fxyz(0, b1) - R.fxyz(0, b1 - 1);
+      const int fr = (b1 % 2 == 0) ? F_RFR : F_LFR;
+      if (b1 % 2 == 0)
+        R.D(fr + c * 3 + 0) = -0.065 * (1 - cos(2 * M_PI / (tsb) * (ph)));
+      else
+        R.D(fr + c * 3 + 0) = 0.075 * (1 - cos(2 * M_PI / (tsb) * (ph)));
+      if (ph >= (tsb / 2)) {
+        if (dx > 0) R.D(fr + c * 3 + 1) = 0.075 * dx / (FOOTX_MAX) * (cos(4 * M_PI / (tsb) * (ph)) - 1);
+      } else {
+        R.D(fr + c * 3 + 1) = 0;
+      }
+    }
+    R.D(F_FTHETA + 0 + 6 * c) = R.D(F_RFR + c * 3 + 0);
+    R.D(F_FTHETA + 1 + 6 * c) = R.D(F_RFR + c * 3 + 1);
+    R.D(F_FTHETA + 2 + 6 * c) = R.D(F_RFR + 2);
+    R.D(F_FTHETA + 3 + 6 * c) = R.D(F_LFR + c * 3 + 0);
+    R.D(F_FTHETA + 4 + 6 * c) = R.D(F_LFR + c * 3 + 1);
+    R.D(F_FTHETA + 5 + 6 * c) = R.D(F_LFR + 2);
+  }
+}
+
+__device__ __forceinline__ void copy3(const Robot &R, int dst, int src) {
+  for (int k = 0; k < 3; ++k) R.D(dst + k) = R.D(src + k);
+}
+
+// xget_position_interpolation (gait_fast.cpp:113-372), live vectors only
+__device__ void interpolation(const RtArgs &a, const Robot &R, const double *g, int flag,
+                              int t_int, int t_end) {
+  int cnt = R.I(I_INT) + 1;
+  if (t_int > 2) {
+    position_mod3(a, R, cnt, F_COM, F_RPY, t_end);
+    position_mod3(a, R, cnt, F_ACC, F_CACC, t_end);
+    position_mod3(a, R, cnt, F_ZMP, F_ZINT, t_end);
+    position_mod3(a, R, cnt, F_DCM, F_DINT, t_end);
+  }
+  if (cnt % 2 == 0) {  // n_t_int = floor(0.025 / 0.01) = 2
+    copy3(R, F_COM + 0, F_COM + 3);
+    copy3(R, F_COM + 3, F_COM + 6);
+    copy3(R, F_ZMP + 0, F_ZMP + 3);
+    copy3(R, F_ZMP + 3, F_ZMP + 6);
+    copy3(R, F_DCM + 0, F_DCM + 3);
+    copy3(R, F_DCM + 3, F_DCM + 6);
+    copy3(R, F_ACC + 0, F_ACC + 3);
+    copy3(R, F_ACC + 3, F_ACC + 6);
+    const double dt = DT_SLOW;
+    if (flag > R.I(I_FLAGOLD)) {  // :170-250
+      for (int k = 0; k < 3; ++k) {
+        R.D(F_COM + 6 + k) = g[k];
+        R.D(F_COM + 12 + k) = g[36 + k];
+        R.D(F_COM + 9 + k) = R.D(F_COM + 6 + k) + R.D(F_COM + 12 + k) * dt;
+        R.D(F_ACC + 6 + k) = g[39 + k];
+        R.D(F_ACC + 9 + k) = g[80 + k];
+      }
+      R.D(F_ZMP + 6) = g[12];
+      R.D(F_ZMP + 7) = g[13];
+      R.D(F_ZMP + 9) = g[42];
+      R.D(F_ZMP + 10) = g[43];
+      R.D(F_DCM + 6) = g[34];
+      R.D(F_DCM + 7) = g[35];
+      R.D(F_DCM + 9) = g[44];
+      R.D(F_DCM + 10) = g[45];
+    } else {  // :251-367
+      for (int k = 0; k < 3; ++k) {
+        double ref = g[k], v = g[36 + k];
+        ref += v * dt;
+        v += g[39 + k] * dt;
+        R.D(F_COM + 6 + k) = ref;
+        R.D(F_COM + 12 + k) = v;
+        R.D(F_COM + 9 + k) = ref + v * dt;
+        R.D(F_ACC + 6 + k) = g[80 + k];
+        R.D(F_ACC + 9 + k) = g[83 + k];
+      }
+      R.D(F_ZMP + 6) = g[42];
+      R.D(F_ZMP + 7) = g[43];
+      R.D(F_ZMP + 9) = g[76];
+      R.D(F_ZMP + 10) = g[77];
+      R.D(F_DCM + 6) = g[44];
+      R.D(F_DCM + 7) = g[45];
+      R.D(F_DCM + 9) = g[78];
+      R.D(F_DCM + 10) = g[79];
+    }
+    cnt = 0;
+    R.I(I_FLAGOLD) = flag;
+  }
+  R.I(I_INT) = cnt;
+}
+
+__global__ __launch_bounds__(256) void rt_pre_kernel(const RtArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t B = a.B;
+  if (r >= B) return;
+  const Ws L = layout(B);
+  Robot R{reinterpret_cast<double *>(a.ws + L.d) + r, reinterpret_cast<int32_t *>(a.ws + L.n) + r, B};
+  double *body = reinterpret_cast<double *>(a.ws + L.body) + r * QLOCO_BODY_STATE_LEN;
+  int32_t *run = reinterpret_cast<int32_t *>(a.ws + L.run) + r;
+  int32_t *bi = reinterpret_cast<int32_t *>(a.ws + L.bi) + r;
+  const double *g = a.gait + r * QLOCO_GAIT_MSG_LEN;
+  const double *ctrl = a.ctrl + r * QLOCO_CTRL_MSG_LEN;
+  // callbacks (:79-110)
+  const int flag = (int)g[99];
+  double nrt[9];
+  for (int k = 0; k < 9; ++k) nrt[k] = g[86 + k];
+  double *bas = reinterpret_cast<double *>(a.ws + L.bas) + r * 4;
+  bas[0] = ctrl[10];
+  bas[1] = ctrl[11];
+  bas[2] = ctrl[13];
+  bas[3] = ctrl[14];
+  int do_body = 0;
+  if (ctrl[0] > 0) {
+    const int loop = R.I(I_LOOP) + 1;
+    R.I(I_LOOP) = loop;
+    const int t_int = (int)((uint32_t)R.I(I_TINT) + (uint32_t)(int)floor((double)(loop / 2)));
+    R.I(I_TINT) = t_int;
+    R.D(F_NRT + 0) = t_int;  // state_to_MPC = state_feedback (:519-527)
+    for (int k = 1; k < 25; ++k) R.D(F_NRT + k) = ctrl[k];
+    if (flag > 0) {
+      const int mpc = R.I(I_MPC) + 1;
+      R.I(I_MPC) = mpc;
+      int t_end = R.I(I_TEND);
+      interpolation(a, R, g, flag, t_int, t_end);
+      if (mpc * DT_FAST > 1.0) {  // _height_offset_timex = 1 (:537-545)
+        const int foot_i = (int)(mpc - (int)1.0 / DT_FAST);
+        int bjx1 = (int)body[26], bjxx = R.I(I_BJXX);
+        foot_traj_mod2(R, foot_i, nrt, bjx1, bjxx, t_end);
+        foot_rotation(R, foot_i, bjx1, bjxx, t_end);
+        body[26] = bjx1;
+        R.I(I_BJXX) = bjxx;
+        R.I(I_TEND) = t_end;
+      }
+      R.D(F_ZMP + 8) = 0.0;  // zmpxyz_ref(2) = _Zsc = {l,r}foot_inter(2) = 0 (:557-566)
+      // body_theta_mpc references (:568-616), Eigen col-major 2x5 / 3x5
+      double *zmp = reinterpret_cast<double *>(a.ws + L.zmp) + r * 10;
+      double *ang = reinterpret_cast<double *>(a.ws + L.ang) + r * 10;
+      double *rft = reinterpret_cast<double *>(a.ws + L.rft) + r * 10;
+      double *lft = reinterpret_cast<double *>(a.ws + L.lft) + r * 10;
+      double *acc = reinterpret_cast<double *>(a.ws + L.acc) + r * 15;
+      for (int j = 0; j < 5; ++j) {
+        if (j == 0) {
+          zmp[0] = R.D(F_ZINT + 0);
+          zmp[1] = R.D(F_ZINT + 1);
+        } else {
+          zmp[2 * j] = R.D(F_ZINT + 8 + 3 * j - 2);
+          zmp[2 * j + 1] = R.D(F_ZINT + 8 + 3 * j - 1);
+        }
+        rft[2 * j] = R.D(F_FOORPR + j * 6 + 1);  // row 0 assigned twice, x then y
+        rft[2 * j + 1] = 0.0;                    // row 1 never assigned
+        lft[2 * j] = R.D(F_FOORPR + j * 6 + 3);
+        lft[2 * j + 1] = R.D(F_FOORPR + j * 6 + 4);
+        ang[2 * j] = (R.D(F_FTHETA + j * 6) + R.D(F_FTHETA + j * 6 + 3)) / 5;
+        ang[2 * j + 1] = (R.D(F_FTHETA + j * 6 + 1) + R.D(F_FTHETA + j * 6 + 4)) / 5;
+        acc[3 * j] = 0.0;
+        acc[3 * j + 1] = 0.0;
+        acc[3 * j + 2] = (j == 0) ? R.D(F_CACC + 2) : R.D(F_CACC + 8 + 3 * j);
+      }
+      R.D(F_BTHX + 0) = ang[0];
+      R.D(F_BTHX + 1) = ang[1];
+      *bi = mpc;
+      do_body = 1;
+    }
+  }
+  *run = do_body;
+}
+
+__global__ __launch_bounds__(256) void rt_post_kernel(const RtArgs a) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t B = a.B;
+  if (r >= B) return;
+  const Ws L = layout(B);
+  Robot R{reinterpret_cast<double *>(a.ws + L.d) + r, reinterpret_cast<int32_t *>(a.ws + L.n) + r, B};
+  const double *body = reinterpret_cast<const double *>(a.ws + L.body) + r * QLOCO_BODY_STATE_LEN;
+  const int32_t run = *(reinterpret_cast<const int32_t *>(a.ws + L.run) + r);
+  const int32_t bst = *(reinterpret_cast<const int32_t *>(a.ws + L.st) + r);
+  const double *g = a.gait + r * QLOCO_GAIT_MSG_LEN;
+  const double *ctrl = a.ctrl + r * QLOCO_CTRL_MSG_LEN;
+  double *t = a.traj + r * QLOCO_TRAJ_MSG_LEN;
+  // /rtMPC/traj: [0,36) = /MPC/Gait[0,36), [36,87) = low_mpc_gait_inte (:633-724)
+  for (int k = 0; k < 36; ++k) t[k] = g[k];
+  double *u = t + 36;
+  for (int k = 0; k < 3; ++k) u[k] = R.D(F_RPY + k);
+  u[3] = R.D(F_BTHX + 0);
+  u[4] = R.D(F_BTHX + 1);
+  u[5] = 0.0;
+  u[6] = R.D(F_FOORPR + 3);
+  u[7] = R.D(F_FOORPR + 4);
+  u[8] = R.D(F_FOORPR + 5);
+  u[9] = R.D(F_FOORPR + 0);
+  u[10] = R.D(F_FOORPR + 1);
+  u[11] = R.D(F_FOORPR + 2);
+  u[12] = R.D(F_ZINT + 0);
+  u[13] = R.D(F_ZINT + 1);
+  u[14] = R.D(F_ZMP + 8);
+  for (int k = 15; k < 27; ++k) u[k] = 0.0;  // F_L, F_R, M_L, M_R
+  u[27] = g[27];
+  u[28] = R.D(F_FTHETA + 3);
+  u[29] = R.D(F_FTHETA + 4);
+  u[30] = R.D(F_FTHETA + 5);
+  u[31] = R.D(F_FTHETA + 0);
+  u[32] = R.D(F_FTHETA + 1);
+  u[33] = R.D(F_FTHETA + 2);
+  u[34] = R.D(F_DINT + 0);
+  u[35] = R.D(F_DINT + 1);
+  // bodyangle_mpc = body_theta_mpc's return = the record's last com_traj
+  for (int k = 0; k < 14; ++k) u[36 + k] = body[12 + k];
+  u[50] = 0.0;                                           // t_fast_mpc (wall clock)
+  for (int k = 87; k < 98; ++k) t[k] = 0.0;
+  t[98] = (int)R.D(F_TXTOT) / 0.001;  // (int) _tx_total / gait::t_program_cyclic
+  t[99] = R.I(I_LOOP);
+  double *n = a.nrt + r * QLOCO_NRT_MSG_LEN;
+  for (int k = 0; k < 25; ++k) n[k] = R.D(F_NRT + k);
+  if (a.gen) {
+    double *o = a.gen + r * 60;
+    for (int k = 0; k < 30; ++k) o[k] = R.D(F_FOORPR + k);
+    for (int k = 0; k < 30; ++k) o[30 + k] = R.D(F_FTHETA + k);
+  }
+  if (a.sched) {
+    int32_t *s = a.sched + r * QLOCO_RT_SCHED_LEN;
+    s[0] = (int32_t)body[26];
+    s[1] = R.I(I_BJXX);
+    s[2] = R.I(I_TEND);
+    s[3] = R.I(I_MPC);
+    s[4] = R.I(I_TINT);
+    s[5] = run ? bst : -1;
+    s[6] = ctrl[0] > 0 ? 1 : 0;
+    s[7] = (int32_t)body[27];
+  }
+}
+
+// PRMPCClass() + Initialize() + gait_fast.cpp main() init (:384-502)
+__global__ __launch_bounds__(256) void rt_init_kernel(int64_t B, char *ws) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= B) return;
+  const Ws L = layout(B);
+  Robot R{reinterpret_cast<double *>(ws + L.d) + r, reinterpret_cast<int32_t *>(ws + L.n) + r, B};
+  for (int f = 0; f < F_DOUBLES; ++f) R.D(f) = 0.0;
+  for (int f = 0; f < I_INTS; ++f) R.I(f) = 0;
+  double *body = reinterpret_cast<double *>(ws + L.body) + r * QLOCO_BODY_STATE_LEN;
+  for (int k = 0; k < QLOCO_BODY_STATE_LEN; ++k) body[k] = 0.0;
+  body[29] = 1.0;  // qp_solution
+  // FootStepInputs(2 * half_hip, 0, 0, 0.015) (:48-53, :2198-2222)
+  const double lift = 0.015;
+  for (int i = 0; i < NS; ++i) R.D(F_LIFT + i) = lift;
+  R.D(F_LIFT + NS - 1) = 0;
+  R.D(F_LIFT + NS - 2) = 0;
+  R.D(F_LIFT + NS - 3) = lift / 2;
+  R.D(F_LIFT + NS - 4) = lift;
+  double fy = 0;  // _footxyz_real (:111-123); x and z stay 0 (steplength = stepheight = 0)
+  for (int i = 1; i < NS; i++) {
+    const double sw = (i - 1 == 0) ? STEPWIDTH0 : 2 * HALF_HIP;
+    fy = fy + (int)pow(-1.0, (double)(i - 1)) * sw;
+    R.fxyz(1, i) = fy;
+  }
+  for (int k = 0; k < 6; ++k) {  // :131-138
+    R.foot(LY, k) = STEPWIDTH0;
+    R.foot(RY, k) = -STEPWIDTH0;
+  }
+  for (int i = 0; i < NS; ++i) R.D(F_TS + i) = TSTEP;  // :168-185
+  recompute_tx(R);
+  R.I(I_TEND) = (int)round((R.D(F_TX + NS - 1) - 3 * TSTEP) / DT_FAST);
+  R.D(F_TXTOT) = R.D(F_TX + NS - 1);
+  const double z_c = 0.309458;  // gait::RobotPara_Z_C (gait_fast.cpp:391-395)
+  R.D(F_COM + 2) = R.D(F_COM + 5) = R.D(F_COM + 8) = R.D(F_COM + 11) = z_c;
+  R.D(F_RPY + 2) = z_c;
+  for (int j = 0; j < 5; j++) {  // :492-496
+    R.D(F_FOORPR + 1 + 6 * j) = -HALF_HIP;
+    R.D(F_FOORPR + 4 + 6 * j) = HALF_HIP;
+  }
+}
+
+static void aaa_inv_mod(double out[16]) {  // :1344-1362
+  const double t[4] = {-DT_SLOW, 0, DT_SLOW, 2 * DT_SLOW};
+  double A[16], Ai[16];
+  for (int r = 0; r < 4; ++r) {
+    A[r * 4 + 0] = cube(t[r]);
+    A[r * 4 + 1] = sq(t[r]);
+    A[r * 4 + 2] = (t[r]);
+    A[r * 4 + 3] = 1;
+  }
+  inv4(A, Ai);
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) out[c * 4 + r] = Ai[r * 4 + c];
+}
+
+}  // namespace rt
+}  // namespace qloco
+
+using namespace qloco;
+
+extern "C" int64_t qloco_rt_workspace_bytes(int64_t batch) {
+  if (batch < 0) return -1;
+  return rt::layout(batch).total;
+}
+
+extern "C" int qloco_rt_init(int64_t batch, void *workspace, void *stream) {
+  if (batch < 0 || (batch > 0 && !workspace)) return QLOCO_ERR_ARG;
+  if (batch == 0) return QLOCO_OK;
+  hipLaunchKernelGGL(rt::rt_init_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, batch, (char *)workspace);
+  QLOCO_HIP_CHECK(hipGetLastError(), "rt_init_kernel launch");
+  return QLOCO_OK;
+}
+
+extern "C" int qloco_rt_tick(int64_t batch, void *workspace, const double *gait_msg,
+                             const double *ctrl_msg, double *traj_msg, double *nrt_msg,
+                             double *gen, int32_t *sched, void *stream) {
+  if (batch < 0) return QLOCO_ERR_ARG;
+  if (batch == 0) return QLOCO_OK;
+  if (!workspace || !gait_msg || !ctrl_msg || !traj_msg || !nrt_msg) return QLOCO_ERR_ARG;
+  if (batch > (int64_t)0x7fffffff * 64) return QLOCO_BAD_SIZE;
+  rt::RtArgs a;
+  memset(&a, 0, sizeof(a));
+  a.B = batch;
+  a.ws = (char *)workspace;
+  a.gait = gait_msg;
+  a.ctrl = ctrl_msg;
+  a.traj = traj_msg;
+  a.nrt = nrt_msg;
+  a.gen = gen;
+  a.sched = sched;
+  rt::aaa_inv_mod(a.aaa_inv_mod);
+  const hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)((batch + 255) / 256));
+  hipLaunchKernelGGL(rt::rt_pre_kernel, grid, dim3(256), 0, s, a);
+  QLOCO_HIP_CHECK(hipGetLastError(), "rt_pre_kernel launch");
+  const rt::Ws L = rt::layout(batch);
+  char *w = (char *)workspace;
+  const int rc = body_mpc_launch(
+      batch, (const int32_t *)(w + L.bi), (const double *)(w + L.bas),
+      (const double *)(w + L.zmp), (const double *)(w + L.ang), (const double *)(w + L.rft),
+      (const double *)(w + L.lft), (const double *)(w + L.acc), (double *)(w + L.body),
+      (double *)(w + L.ct), (int32_t *)(w + L.st),
+      (const double *)(w + L.d) + (int64_t)rt::F_TX * batch, batch,
+      (const int32_t *)(w + L.run), s);
+  if (rc != QLOCO_OK) return rc;
+  hipLaunchKernelGGL(rt::rt_post_kernel, grid, dim3(256), 0, s, a);
+  QLOCO_HIP_CHECK(hipGetLastError(), "rt_post_kernel launch");
+  return QLOCO_OK;
+}

@@ -1,0 +1,160 @@
+"""Batched rt_mpc_qp node tick on gfx950.
+
+`RtNodeBatch.tick(gait_msg, ctrl_msg)` runs one iteration of the rt node's
+100 Hz loop (unitree_ros/rt_mpc_qp/src/gait_fast.cpp:505-735) for B robots:
+the subscriber callbacks on the latest /MPC/Gait (100 doubles) and
+/control2rtmpc/state (25 doubles) messages, the reference interpolation,
+the contact-schedule / swing-foot / foot-rotation generators of PRMPCClass
+and body_theta_mpc, and returns the /rtMPC/traj (100) and /rt2nrt/state (25)
+messages.  Member state stays on the device (one workspace per batch).
+
+`synth_messages` produces deterministic wire-format traffic for tests and
+the benchmark (there is no recorded ROS traffic in the reference): a slow
+planner publishing at 40 Hz with the layout of NLPRTControlClass.cpp:284-392
+(Nrtfoorpr_gen from NLPClass_sqp.cpp:1079-1087) and a servo state stream.
+"""
+import numpy as np
+
+from ._lib import check, lib, ptr
+
+GAIT_LEN, CTRL_LEN, TRAJ_LEN, NRT_LEN, SCHED_LEN = 100, 25, 100, 25, 8
+
+
+def _stream(t):
+    import ctypes as C
+
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+class RtNodeBatch:
+    """B rt_mpc_qp nodes (PRMPCClass + gait_fast.cpp globals) on one device."""
+
+    def __init__(self, batch, device="cuda:0"):
+        import torch
+        self.batch = int(batch)
+        self.device = torch.device(device)
+        nbytes = int(lib().qloco_rt_workspace_bytes(self.batch))
+        if nbytes < 0:
+            raise ValueError("bad batch %d" % batch)
+        self.ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+        f64 = dict(dtype=torch.float64, device=self.device)
+        self.traj = torch.zeros((self.batch, TRAJ_LEN), **f64)
+        self.nrt = torch.zeros((self.batch, NRT_LEN), **f64)
+        self.gen = torch.zeros((self.batch, 60), **f64)
+        self.sched = torch.zeros((self.batch, SCHED_LEN), dtype=torch.int32, device=self.device)
+        check(lib().qloco_rt_init(self.batch, ptr(self.ws), _stream(self.ws)), "qloco_rt_init")
+
+    def tick(self, gait_msg, ctrl_msg, with_debug=True, stream=None):
+        """One loop iteration; gait_msg (B,100), ctrl_msg (B,25) float64 device
+        tensors.  Returns (traj, nrt, gen, sched) device tensors (reused)."""
+        s = _stream(self.ws) if stream is None else stream
+        check(lib().qloco_rt_tick(self.batch, ptr(self.ws), ptr(gait_msg), ptr(ctrl_msg),
+                                  ptr(self.traj), ptr(self.nrt),
+                                  ptr(self.gen) if with_debug else None,
+                                  ptr(self.sched) if with_debug else None, s), "qloco_rt_tick")
+        return self.traj, self.nrt, self.gen, self.sched
+
+
+def _u(seed, b, field):
+    """counter-based uniform [0,1) per (seed, robot, field), vectorised over b"""
+    with np.errstate(over="ignore"):  # mod-2^64 arithmetic (splitmix64 finaliser)
+        x = (np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15)
+             + b.astype(np.uint64) * np.uint64(0xBF58476D1CE4E5B9)
+             + np.uint64(field) * np.uint64(0x94D049BB133111EB))
+        x ^= x >> np.uint64(30)
+        x *= np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(31)
+    return (x >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+
+
+_CONSTS = {}
+
+
+def _robot_consts(seed, first, batch):
+    """memoised per-robot uniforms U(field) for one (seed, first, batch)"""
+    key = (seed, first, batch)
+    if key not in _CONSTS:
+        if len(_CONSTS) > 64:
+            _CONSTS.clear()
+        b = np.arange(first, first + batch, dtype=np.int64)
+        cache = {}
+
+        def U(f):
+            if f not in cache:
+                if isinstance(f, tuple):  # ("c"|"s", field): cos / sin of 2*pi*U(field)
+                    ph = 6.28 * U(f[1])
+                    cache[f] = np.cos(ph) if f[0] == "c" else np.sin(ph)
+                else:
+                    cache[f] = _u(seed, b, f)
+            return cache[f]
+        _CONSTS[key] = U
+    return _CONSTS[key]
+
+
+def synth_messages(seed, batch, tick, first=0):
+    """(gait_msg, ctrl_msg) float64 arrays (B,100), (B,25) for loop tick `tick`.
+
+    Per robot: start delay 0..3 ticks on /control2rtmpc/state[0]; a planner
+    message index m = floor(tick * 0.01 / 0.025) (40 Hz vs 100 Hz); step
+    index bjxx = floor(t_nlp / T) + 1 with a per-robot step period T (half
+    the robots also send it as ts, Nrtfoorpr_gen[8]); footholds advance by
+    a per-robot step length with the reference's alternating y pattern;
+    /MPC/Gait[99] is a per-message counter for 3/4 of the robots (new-data
+    branch of xget_position_interpolation) and the planner's right_support
+    (0/1/2) for the rest.  COM/ZMP/DCM references are smooth functions of
+    the planner time plus per-robot offsets.
+    """
+    U = _robot_consts(int(seed), int(first), int(batch))
+    start = np.floor(U(1) * 4)
+    period = 0.6 + 0.2 * U(2)                # step period T
+    send_ts = U(3) < 0.5
+    steplen = 0.08 * U(4)
+    counter_flag = U(5) < 0.75
+    vx = steplen / period
+    m = np.floor(tick * 0.01 / 0.025)        # planner message index
+    t_nlp = m * 0.025
+    gait = np.zeros((GAIT_LEN, batch))  # field-major while filling
+    ctrl = np.zeros((CTRL_LEN, batch))
+    ctrl[0] = (tick >= start).astype(np.float64)
+    # sin(a + c) = sin(a) cos(c) + cos(a) sin(c): per-tick scalars a, cached
+    # per-robot phases c -- no per-robot transcendental per column
+    for k in range(1, CTRL_LEN):
+        a = 0.37 * tick + 1.3 * k
+        ctrl[k] = 0.05 * (np.sin(a) * U(("c", 100 + k)) + np.cos(a) * U(("s", 100 + k)))
+    ph = 2 * np.pi * t_nlp / period
+    sph, cph = np.sin(ph), np.cos(ph)
+    sh, ch = np.sin(ph / 2), np.cos(ph / 2)
+    gait[0] = vx * t_nlp + 0.01 * U(10)
+    gait[1] = 0.02 * sh
+    gait[2] = 0.309458 + 0.005 * sph
+    gait[36] = vx
+    gait[37] = 0.02 * np.pi / period * ch
+    gait[38] = 0.005 * 2 * np.pi / period * cph
+    for k in (39, 40, 41, 80, 81, 82, 83, 84, 85):
+        gait[k] = 0.3 * (sph * np.cos(k) + cph * np.sin(k))
+    for k in (12, 13, 34, 35, 42, 43, 44, 45, 76, 77, 78, 79):
+        gait[k] = 0.03 * (sph * np.cos(0.5 * k) + cph * np.sin(0.5 * k)) + (
+            0.0 if k % 2 else vx * t_nlp)
+    for k in list(range(3, 12)) + list(range(14, 27)) + list(range(28, 34)) + list(range(46, 76)):
+        a = 0.1 * m + k
+        gait[k] = 0.01 * (np.sin(a) * U(("c", 200 + k)) + np.cos(a) * U(("s", 200 + k)))
+    bjxx = np.minimum(np.floor(np.maximum(t_nlp - 1.0, 0.0) / period) + 1, 25)
+    gait[27] = bjxx
+    fy = lambda i: np.where(i % 2 == 1, 0.12675, -0.12675)
+    gait[86] = bjxx
+    gait[87] = bjxx * steplen
+    gait[88] = (bjxx + 1) * steplen
+    gait[89] = fy(bjxx) + 0.01 * (U(6) - 0.5)
+    gait[90] = fy(bjxx + 1) + 0.01 * (U(7) - 0.5)
+    gait[91] = 0.005 * U(8)
+    gait[92] = 0.005 * U(9)
+    gait[93] = bjxx - 1
+    gait[94] = np.where(send_ts, period, 0.0)
+    gait[97] = 0.0
+    gait[98] = 1e-4
+    right_support = np.where(bjxx < 2, 2, bjxx % 2)
+    gait[99] = np.where(counter_flag, m + 1, right_support)
+    return np.ascontiguousarray(gait.T), np.ascontiguousarray(ctrl.T)

@@ -142,8 +142,60 @@ def lib():
         L.qo_body_theta_mpc.restype = C.c_int
         L.qo_body_theta_mpc.argtypes = [C.POINTER(BodyState), C.c_int, dp, dp, dp, dp, dp,
                                         dp, dp, dp, ip]
+        L.qo_rt_create_n.restype = C.c_void_p
+        L.qo_rt_create_n.argtypes = [C.c_int64]
+        L.qo_rt_destroy_n.argtypes = [C.c_void_p, C.c_int64]
+        L.qo_rt_tick_n.argtypes = [C.c_void_p, C.c_int64] + [C.c_void_p] * 6
+        L.qo_inv4.argtypes = [dp, dp]
         _lib = L
     return _lib
+
+
+class RtOracle:
+    """B rt_mpc_qp nodes in the C restatement (oracle/rt_tick.c)."""
+    SCHED = 8
+
+    def __init__(self, batch):
+        self.batch = batch
+        self.h = lib().qo_rt_create_n(batch)
+
+    def tick(self, gait, ctrl):
+        B = self.batch
+        gait = np.ascontiguousarray(gait, np.float64)
+        ctrl = np.ascontiguousarray(ctrl, np.float64)
+        traj, nrt = np.zeros((B, 100)), np.zeros((B, 25))
+        gen, sched = np.zeros((B, 60)), np.zeros((B, self.SCHED), np.int32)
+        lib().qo_rt_tick_n(self.h, B, gait.ctypes.data, ctrl.ctypes.data, traj.ctypes.data,
+                           nrt.ctypes.data, gen.ctypes.data, sched.ctypes.data)
+        return traj, nrt, gen, sched
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().qo_rt_destroy_n(self.h, self.batch)
+            self.h = None
+
+
+class BodyStep:
+    """body_theta_mpc of the C restatement on a caller-supplied _tx / _bjx1
+    (the per-robot members the rt generators rewrite) -- for tests/rt_ref.py."""
+
+    def __init__(self):
+        self.s = BodyState()
+        lib().qo_body_init(C.byref(self.s))
+
+    def __call__(self, i, bodyangle_state, zmp, ang, rfoot, lfoot, acc, tx, bjx1):
+        for j in range(27):
+            self.s.tx[j] = float(tx[j])
+        self.s.bjx1 = int(bjx1)
+        col = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).T.reshape(-1))
+        out = np.zeros(14)
+        st = C.c_int(0)
+        bs = np.ascontiguousarray(bodyangle_state, np.float64)
+        args = [col(zmp), col(ang), col(rfoot), col(lfoot), col(acc)]
+        nrt = np.zeros(9)
+        lib().qo_body_theta_mpc(C.byref(self.s), int(i), P(bs), *[P(a) for a in args], P(nrt),
+                                P(out), C.byref(st))
+        return out, self.s.bjx1, st.value
 
 
 def P(a, t=C.c_double):

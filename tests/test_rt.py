@@ -1,0 +1,103 @@
+"""rt_mpc_qp node tick: oracle pinning on the CPU.
+
+The C restatement (oracle/rt_tick.c) is held to an independent Python
+transcription of the same reference lines (tests/rt_ref.py) over a long
+synthetic run that walks every branch of Foot_trajectory_solve_mod2 and
+XGetSolution_Foot_rotation: double support, swing, touchdown snap, the
+step-period rewrite from Nrtfoorpr_gen[8], and the post-schedule stop
+branch (j_index > _t_end_footstep).  Everything must be bit-identical: the
+two transcriptions share only the numeric primitives the reference leaves to
+Eigen/libm (4x4 Gauss-Jordan inverse, compensated cube, index-order sums).  The committed fixture tests/golden/rt_tick.npz (made by
+tests/golden/make_rt_golden.py from the C restatement) is replayed too.
+
+Parity with the reference binary is unpinned (it needs Eigen/Armadillo/ROS,
+SURVEY.md §8c); the known quirks are asserted explicitly below.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from quadrupedal_loco_amd.rt import synth_messages
+from rt_ref import RtNode
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SEED = 20261016
+
+
+def _run_pair(B, T, seed=SEED):
+    orc = O.RtOracle(B)
+    ref = [RtNode(O.BodyStep()) for _ in range(B)]
+    hist = {"swing": 0, "ds": 0, "stop": 0, "body": 0, "maxdiff": 0.0}
+    for t in range(T):
+        gait, ctrl = synth_messages(seed, B, t)
+        traj, nrt, gen, sched = orc.tick(gait, ctrl)
+        for b in range(B):
+            rt, rn, rg, rs = ref[b].tick(gait[b], ctrl[b])
+            assert list(sched[b, :7]) == list(rs), (t, b, sched[b], rs)
+            for name, a, r in (("traj", traj[b], rt), ("nrt", nrt[b], rn), ("gen", gen[b], rg)):
+                # bit-exact: same primitives (inv4, cube, index-order sums, glibc cos)
+                d = np.abs(a - r)
+                assert np.array_equal(a, r), (t, b, name, int(np.argmax(d)), a[np.argmax(d)],
+                                              r[np.argmax(d)])
+                hist["maxdiff"] = max(hist["maxdiff"], float(d.max()))
+            if rs[5] >= 0:
+                hist["body"] += 1
+            if rs[3] - 100 > rs[2]:
+                hist["stop"] += 1
+        for b in range(B):
+            # swing branch: a foot z above its hold value
+            if np.any(np.abs(gen[b, [2, 5, 8, 11]]) > 1e-4):
+                hist["swing"] += 1
+    return hist
+
+
+def test_rt_oracle_matches_transcription():
+    hist = _run_pair(B=4, T=1900)
+    assert hist["body"] > 4000
+    assert hist["swing"] > 1000
+    assert hist["stop"] > 0, "run too short to reach the post-schedule branch"
+
+
+def test_rt_initial_messages_and_quirks():
+    """Tick 0 with the loop not started, then the reference's fixed quirks."""
+    orc = O.RtOracle(2)
+    gait = np.zeros((2, 100))
+    ctrl = np.zeros((2, 25))
+    traj, nrt, gen, sched = orc.tick(gait, ctrl)
+    # not started: no /rt2nrt/state, traj carries the init values
+    assert np.all(sched[:, 6] == 0) and np.all(sched[:, 5] == -1)
+    assert np.all(nrt == 0)
+    assert np.allclose(traj[:, 36 + 2], 0.309458)  # rpy_mpc_body(2) = COM_ref2(2)
+    assert np.allclose(traj[:, 36 + 7], 0.12675) and np.allclose(traj[:, 36 + 10], -0.12675)
+    # [98] = (int)_tx_total / t_program_cyclic with _tx_total = 26 * 0.7 - 1e-5
+    assert traj[0, 98] == 18.0 / 0.001
+    ctrl[:, 0] = 1
+    gait[:, 99] = 1
+    for t in range(130):
+        traj, nrt, gen, sched = orc.tick(gait, ctrl)
+    # t_int = sum_{c=1..130} floor(c/2); state_to_MPC[0] = t_int
+    assert sched[0, 4] == sum(c // 2 for c in range(1, 131)) == nrt[0, 0]
+    assert traj[0, 99] == 130 and sched[0, 3] == 130
+    # foot generation starts when count_in_rt_mpc * 0.01 > 1 (count 101)
+    assert sched[0, 5] >= 0
+
+
+def test_rt_golden_replay():
+    path = os.path.join(HERE, "golden", "rt_tick.npz")
+    z = np.load(path)
+    B, T = int(z["batch"]), int(z["ticks"])
+    orc = O.RtOracle(B)
+    k = 0
+    for t in range(T):
+        gait, ctrl = synth_messages(int(z["seed"]), B, t)
+        traj, nrt, gen, sched = orc.tick(gait, ctrl)
+        if t in z["ticks_saved"]:
+            np.testing.assert_array_equal(gait, z["gait"][k])
+            np.testing.assert_array_equal(ctrl, z["ctrl"][k])
+            np.testing.assert_array_equal(traj, z["traj"][k])
+            np.testing.assert_array_equal(nrt, z["nrt"][k])
+            np.testing.assert_array_equal(sched, z["sched"][k])
+            k += 1
+    assert k == len(z["ticks_saved"])

@@ -1,0 +1,114 @@
+"""Measurement for SURVEY.md §8f rows 2-3 (batched rt_mpc_qp node tick): one
+JSON line with robot-ticks/s, the HBM roofline of a tick and the C
+restatement timed beside it.
+
+    python tools/bench_rt.py [--robots B] [--steps K] [--warmup W] [--sets M]
+
+Workload: B robots (default 65536), one qloco_rt_tick per step = the rt
+node's 100 Hz loop body for every robot (gait_fast.cpp:505-735: callbacks,
+interpolation, Foot_trajectory_solve_mod2, XGetSolution_Foot_rotation,
+body_theta_mpc, /rtMPC/traj + /rt2nrt/state).  M message sets
+(synth_messages for ticks 0..M-1) are generated on the host and resident in
+HBM before the timed region; step t uses set t mod M.  W warm-up ticks
+(default 150) run first so every robot is past the 1 s height-offset phase
+and into foot generation + body MPC (count_in_rt_mpc > 100).
+Algorithmic HBM bytes per robot-tick (fp64): messages in 125 x 8 = 1000,
+messages out 125 x 8 = 1000, node state read + written 2 x (551 x 8 + 7 x 4
++ 32 x 8) = 9384 -> 11384 B.  Peak 8.0 TB/s (MI355X_MICROARCH.md).
+cpu_baseline: oracle/rt_tick.c (qo_rt_tick_n), 1 thread, bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0
+BYTES_PER_ROBOT_TICK = 1000 + 1000 + 2 * (551 * 8 + 7 * 4 + 32 * 8)
+SEED = 20261016
+
+
+def cpu_baseline(sets, budget_s=8.0):
+    """robot-ticks/s of the C restatement over a bounded sample: 1024 robots
+    warmed up 150 ticks untimed, then timed ticks until the budget."""
+    import oracle_lib as O
+    from quadrupedal_loco_amd.rt import synth_messages
+    n = 1024
+    orc = O.RtOracle(n)
+    M = len(sets)
+    msgs = [synth_messages(SEED, n, t) for t in range(M)]
+    for t in range(150):
+        orc.tick(*msgs[t % M])
+    ticks, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        orc.tick(*msgs[(150 + ticks) % M])
+        ticks += 1
+    dt = time.perf_counter() - t0
+    return n * ticks / dt, "%d robots x %d ticks (after 150 warm-up ticks)" % (n, ticks)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--robots", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=150)
+    ap.add_argument("--sets", type=int, default=40)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    import torch
+    from quadrupedal_loco_amd.rt import RtNodeBatch, synth_messages
+    B, M = args.robots, args.sets
+    dev = torch.device("cuda:0")
+    sets = []
+    for t in range(M):
+        g, c = synth_messages(SEED, B, t)
+        sets.append((torch.from_numpy(g).to(dev), torch.from_numpy(c).to(dev)))
+    node = RtNodeBatch(B, dev)
+    for t in range(args.warmup):
+        node.tick(*sets[t % M], with_debug=False)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for k in range(args.steps):
+        node.tick(*sets[(args.warmup + k) % M], with_debug=False)
+        ev[k + 1].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    per = np.array([ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)])
+    ms = float(per.mean())
+    _, _, _, sched = node.tick(*sets[0])
+    sched = sched.cpu().numpy()
+    achieved = BYTES_PER_ROBOT_TICK * B / (ms * 1e-3) / 1e9
+    line = {"metric": "rt_mpc_qp node ticks/sec (gait_fast loop body + PRMPCClass generators "
+                      "+ body_theta_mpc, fp64)",
+            "value": B / (ms * 1e-3), "unit": "robot-ticks/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "p99_tick_us": float(np.percentile(per, 99) * 1e3),
+            "wall_ms_per_step": wall / args.steps * 1e3,
+            "higher_is_better": True, "dtype": "f64",
+            "data": "synthetic wire-format messages (quadrupedal_loco_amd.rt.synth_messages, "
+                    "%d sets cycled)" % M,
+            "config": {"workload": "rt node tick, %d robots" % B},
+            "body_mpc_ran_frac": float(np.mean(sched[:, 5] >= 0)),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_robot_tick": BYTES_PER_ROBOT_TICK,
+                         "traffic": None,
+                         "note": "whole tick (3 launches) against the state-streaming bytes"}}
+    if not args.no_cpu_baseline:
+        v, sample = cpu_baseline(sets)
+        line["cpu_baseline"] = {"value": v, "unit": "robot-ticks/s", "cores": 1, "kind": "port",
+                                "sample": sample + ", oracle/rt_tick.c"}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
