@@ -20,6 +20,8 @@
  *                                    ConvexMpc (A1RobotControl.cpp:452-600)
  *   Kinematicclass                <- go1_rt_control Kinematicclass
  *                                    (Kinematics.h:30-61; servo.cpp:734-741, :1038-1051)
+ *   RtMpcNode                     <- the rt_mpc_qp node loop (gait_fast.cpp:79-735):
+ *                                    subscriber callbacks + one 100 Hz iteration
  *
  * Every class is batched over B independent robots (B = 1 is the drop-in
  * case).  Host arrays are staged to the device on the object's HIP stream;
@@ -245,6 +247,36 @@ class Kinematicclass {
   double *d_a_, *d_b_, *d_p_, *d_r_, *d_q_, *d_pos_, *d_jac_;
   int32_t *d_leg_, *d_upd_;
   void ensure(int n);
+};
+
+// ------------------------------------------------------------------------
+// The rt_mpc_qp node (unitree_ros/rt_mpc_qp/src/gait_fast.cpp) for B robots:
+// the two subscriber callbacks store the latest /MPC/Gait (100 doubles,
+// :79-89) and /control2rtmpc/state (25 doubles, :92-110) message of a robot;
+// loop_once() runs one iteration of the 100 Hz loop (:505-735) -- reference
+// interpolation, PRMPCClass contact schedule / swing-foot / foot-rotation
+// generators, body_theta_mpc -- for every robot on the GPU (qloco_rt_tick)
+// and leaves the outgoing messages in `traj` (/rtMPC/traj, 100 per robot)
+// and `nrt` (/rt2nrt/state, 25 per robot; valid when published(robot)).
+class RtMpcNode {
+ public:
+  explicit RtMpcNode(int batch = 1);
+  void nrt_gait_sub_operation(const double msg[QLOCO_GAIT_MSG_LEN], int robot = 0);
+  void control_gait_sub_operation(const double msg[QLOCO_CTRL_MSG_LEN], int robot = 0);
+  void loop_once();
+  bool published(int robot = 0) const { return sched[robot * QLOCO_RT_SCHED_LEN + 6] != 0; }
+  std::vector<double> traj;     // B * 100
+  std::vector<double> nrt;      // B * 25
+  std::vector<int32_t> sched;   // B * QLOCO_RT_SCHED_LEN (bjx1, bjxx, t_end, counters, ...)
+  int batch() const { return batch_; }
+
+ private:
+  int batch_;
+  DeviceArena arena_;
+  std::vector<double> gait_, ctrl_;
+  void *d_ws_;
+  double *d_gait_, *d_ctrl_, *d_traj_, *d_nrt_;
+  int32_t *d_sched_;
 };
 
 }  // namespace qloco

@@ -4,6 +4,8 @@
 // HIP stream and calls libqloco.so.  No solver arithmetic lives here except
 // the reference's own input assembly for compute_grf
 // (A1RobotControl.cpp:459-497), which is host-side in the reference too.
+#include <algorithm>
+
 #include "qloco.hpp"
 
 #include <hip/hip_runtime.h>
@@ -550,6 +552,51 @@ std::array<double, 3> Kinematicclass::Inverse_kinematics_g(const double body_P[3
                 Jacobian_kin.data(), &upd);
   last_updates = upd;
   return q;
+}
+
+
+// ---------------------------------------------------------------- RtMpcNode
+RtMpcNode::RtMpcNode(int batch) : batch_(batch) {
+  if (batch < 1) throw Error("RtMpcNode: batch < 1", QLOCO_ERR_ARG);
+  const size_t B = batch;
+  gait_.assign(B * QLOCO_GAIT_MSG_LEN, 0.0);  // low_mpc_gait.setZero() (gait_fast.cpp:387)
+  ctrl_.assign(B * QLOCO_CTRL_MSG_LEN, 0.0);
+  traj.assign(B * QLOCO_TRAJ_MSG_LEN, 0.0);
+  nrt.assign(B * QLOCO_NRT_MSG_LEN, 0.0);
+  sched.assign(B * QLOCO_RT_SCHED_LEN, 0);
+  const int64_t ws = qloco_rt_workspace_bytes(batch);
+  if (ws < 0) throw Error("qloco_rt_workspace_bytes", QLOCO_ERR_ARG);
+  d_ws_ = arena_.alloc((size_t)ws);
+  d_gait_ = dalloc<double>(arena_, B * QLOCO_GAIT_MSG_LEN);
+  d_ctrl_ = dalloc<double>(arena_, B * QLOCO_CTRL_MSG_LEN);
+  d_traj_ = dalloc<double>(arena_, B * QLOCO_TRAJ_MSG_LEN);
+  d_nrt_ = dalloc<double>(arena_, B * QLOCO_NRT_MSG_LEN);
+  d_sched_ = dalloc<int32_t>(arena_, B * QLOCO_RT_SCHED_LEN);
+  abi_ok(qloco_rt_init(batch, d_ws_, arena_.stream()), "qloco_rt_init");
+  arena_.sync();
+}
+
+void RtMpcNode::nrt_gait_sub_operation(const double msg[QLOCO_GAIT_MSG_LEN], int robot) {
+  if (robot < 0 || robot >= batch_) throw Error("RtMpcNode: robot out of range", QLOCO_ERR_ARG);
+  std::copy(msg, msg + QLOCO_GAIT_MSG_LEN, gait_.begin() + (size_t)robot * QLOCO_GAIT_MSG_LEN);
+}
+
+void RtMpcNode::control_gait_sub_operation(const double msg[QLOCO_CTRL_MSG_LEN], int robot) {
+  if (robot < 0 || robot >= batch_) throw Error("RtMpcNode: robot out of range", QLOCO_ERR_ARG);
+  std::copy(msg, msg + QLOCO_CTRL_MSG_LEN, ctrl_.begin() + (size_t)robot * QLOCO_CTRL_MSG_LEN);
+}
+
+void RtMpcNode::loop_once() {
+  const size_t B = batch_;
+  arena_.upload(d_gait_, gait_.data(), sizeof(double) * B * QLOCO_GAIT_MSG_LEN);
+  arena_.upload(d_ctrl_, ctrl_.data(), sizeof(double) * B * QLOCO_CTRL_MSG_LEN);
+  abi_ok(qloco_rt_tick(batch_, d_ws_, d_gait_, d_ctrl_, d_traj_, d_nrt_, nullptr, d_sched_,
+                       arena_.stream()),
+         "qloco_rt_tick");
+  arena_.download(traj.data(), d_traj_, sizeof(double) * B * QLOCO_TRAJ_MSG_LEN);
+  arena_.download(nrt.data(), d_nrt_, sizeof(double) * B * QLOCO_NRT_MSG_LEN);
+  arena_.download(sched.data(), d_sched_, sizeof(int32_t) * B * QLOCO_RT_SCHED_LEN);
+  arena_.sync();
 }
 
 }  // namespace qloco

@@ -8,6 +8,9 @@
 //  2. QPsolverGpu / QPBaseClassGpu on random QPs vs qo_eqp_solve.
 //  3. PRMPCClass::body_theta_mpc over a gait window vs qo_body_theta_mpc;
 //     Indexfind bit-exact.
+//  5. RtMpcNode (gait_fast.cpp loop) over 400 ticks of scripted messages vs
+//     qo_rt_tick_n: schedule integers and /rt2nrt/state bit-exact, /rtMPC/traj
+//     within 1e-9 (foot-rotation cos is the device libm's).
 //  4. ConvexMpcBatch::compute_grf on the inputs of the reference harness
 //     test_mpc.cpp:18-91 (A1, mass 15, contacts FL, RL): forces within 0.5 N
 //     of the exact optimum committed in tests/golden/srbd_test_mpc_kat.npz.
@@ -258,6 +261,56 @@ static void test_kinematics() {
   std::printf("kinematics ok: FK/IK per leg + batch of %d\n", n);
 }
 
+
+static void test_rt_node() {
+  const int B = 3, T = 400;
+  qloco::RtMpcNode node(B);
+  qo_rt *ref = qo_rt_create_n(B);
+  std::vector<double> gait(B * 100, 0.0), ctrl(B * 25, 0.0), traj(B * 100), nrt(B * 25);
+  std::vector<int32_t> sched(B * QO_RT_SCHED);
+  for (int t = 0; t < T; ++t) {
+    for (int b = 0; b < B; ++b) {  // a walking planner stream, started at tick b
+      double *g = &gait[b * 100], *c = &ctrl[b * 25];
+      const double tn = std::floor(t * 0.4) * 0.025;
+      c[0] = t >= b ? 1.0 : 0.0;
+      for (int k = 1; k < 25; ++k) c[k] = 0.03 * std::sin(0.2 * t + k + b);
+      g[0] = 0.05 * tn;
+      g[1] = 0.01 * std::sin(3.0 * tn);
+      g[2] = 0.3;
+      g[36] = 0.05;
+      for (int k : {12, 13, 34, 35, 42, 43, 44, 45, 76, 77, 78, 79}) g[k] = 0.02 * std::cos(tn + k);
+      for (int k : {39, 40, 41, 80, 81, 82, 83, 84, 85}) g[k] = 0.2 * std::sin(2 * tn + k);
+      const double bj = std::fmin(std::floor(std::fmax(tn - 1.0, 0.0) / 0.7) + 1, 25);
+      g[27] = g[86] = bj;
+      g[87] = 0.04 * bj;
+      g[88] = 0.04 * (bj + 1);
+      g[89] = ((int)bj % 2) ? 0.12675 : -0.12675;
+      g[90] = -g[89];
+      g[93] = bj - 1;
+      g[94] = b == 1 ? 0.65 : 0.0;
+      g[99] = std::floor(t * 0.4) + 1;
+      node.nrt_gait_sub_operation(g, b);
+      node.control_gait_sub_operation(c, b);
+    }
+    node.loop_once();
+    qo_rt_tick_n(ref, B, gait.data(), ctrl.data(), traj.data(), nrt.data(), nullptr, sched.data());
+    for (int b = 0; b < B; ++b) {
+      for (int k = 0; k < QO_RT_SCHED; ++k)
+        CHECK(node.sched[b * QLOCO_RT_SCHED_LEN + k] == sched[b * QO_RT_SCHED + k],
+              "rt sched t=%d robot %d [%d] %d vs %d\n", t, b, k, node.sched[b * 8 + k],
+              sched[b * QO_RT_SCHED + k]);
+      for (int k = 0; k < 25; ++k)
+        CHECK(node.nrt[b * 25 + k] == nrt[b * 25 + k], "rt nrt t=%d robot %d [%d]\n", t, b, k);
+      for (int k = 0; k < 100; ++k)
+        CHECK(close(node.traj[b * 100 + k], traj[b * 100 + k], 1e-9, 1e-9),
+              "rt traj t=%d robot %d [%d] %.12g vs %.12g\n", t, b, k, node.traj[b * 100 + k],
+              traj[b * 100 + k]);
+    }
+  }
+  qo_rt_destroy_n(ref, B);
+  std::printf("rt node ok: %d robots x %d ticks\n", B, T);
+}
+
 int main() {
   try {
     test_force_qp();
@@ -265,6 +318,7 @@ int main() {
     test_body_mpc();
     test_convex_mpc();
     test_kinematics();
+    test_rt_node();
   } catch (const qloco::Error &e) {
     std::printf("FAIL: qloco::Error %s (status %d)\n", e.what(), e.status);
     return 2;

@@ -170,8 +170,11 @@ class RtOracle:
         return traj, nrt, gen, sched
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().qo_rt_destroy_n(self.h, self.batch)
+        if getattr(self, "h", None) and _lib is not None:
+            try:
+                _lib.qo_rt_destroy_n(self.h, self.batch)
+            except Exception:  # interpreter teardown
+                pass
             self.h = None
 
 

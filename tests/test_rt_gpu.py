@@ -138,3 +138,27 @@ def test_rt_tick_rejects_bad_args():
     assert lib().qloco_rt_workspace_bytes(-1) < 0
     node = RtNodeBatch(0, dev)  # empty batch is a no-op
     assert node.batch == 0
+
+
+def test_replay_tool_on_gpu(tmp_path):
+    """python -m quadrupedal_loco_amd.replay: a recorded input log through the
+    GPU node matches the oracle's output log."""
+    from quadrupedal_loco_amd.replay import KIND_INPUT, RtLogWriter, read_log, replay
+    dev = _dev()
+    B, T = 16, 300
+    path, opath = str(tmp_path / "in.qlog"), str(tmp_path / "out.qlog")
+    orc = O.RtOracle(B)
+    ref = []
+    with RtLogWriter(path, B, KIND_INPUT) as w:
+        for t in range(T):
+            gait, ctrl = synth_messages(SEED, B, t)
+            w.append(gait, ctrl)
+            traj, nrt, _, _ = orc.tick(gait, ctrl)
+            ref.append((traj, nrt))
+    assert replay(path, opath, str(dev)) == T
+    _, out = read_log(opath)
+    for t in range(T):
+        row = np.array(out[t])  # (B, 125)
+        assert np.array_equal(row[:, EXACT], ref[t][0][:, EXACT]), t
+        assert _close(row[:, :100], ref[t][0]).all(), t
+        assert np.array_equal(row[:, 100:], ref[t][1]), t
