@@ -221,3 +221,23 @@ void qo_compute_joint_torques(const qo_dyn_state *s, const double J[9], int swin
     tau[r] = -acc + (r == 0 ? gcomp[leg_number] : 0.0);
   }
 }
+
+/* Batch driver for the CPU baseline (tools/bench_qp.py): servo.cpp:1224-1228
+ * (force_distribution then force_opt) for n robots, row layout of
+ * qloco_force_qp_solve, one persistent Dynamiccclass per robot in `states`
+ * (n records, qo_dyn_init'ed by the caller).  Single thread. */
+void qo_force_batch(int64_t n, qo_dyn_state *states, const qo_force_params *prm,
+                    const double *com_des, const double *leg_des, const double *F_force_des,
+                    const double *rfoot_des, const double *lfoot_des, const double *base_p,
+                    const double *feet_p, const double *FT_total_des, const int32_t *mode,
+                    const int32_t *right_support, const double *y_coef, double *grf_opt) {
+  for (int64_t b = 0; b < n; ++b) {
+    qo_dyn_state *s = &states[b];
+    qo_force_distribution(s, com_des + 3 * b, leg_des + 12 * b, F_force_des + 6 * b, mode[b],
+                          y_coef[b], rfoot_des + 3 * b, lfoot_des + 3 * b);
+    const double *f = feet_p + 12 * b;
+    qo_force_opt(s, prm, base_p + 3 * b, f, f + 3, f + 6, f + 9, FT_total_des + 6 * b, mode[b],
+                 right_support[b], y_coef[b], NULL, NULL);
+    memcpy(grf_opt + 12 * b, s->grf_opt, sizeof(double) * 12);
+  }
+}

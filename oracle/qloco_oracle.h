@@ -89,6 +89,13 @@ int qo_force_opt(qo_dyn_state *s, const qo_force_params *prm,
                  const double RR_p[3], const double RL_p[3],
                  const double FT_total_des[6], int mode, int right_support,
                  double y_coefficient, int *eqp_status, int *iters);
+/* batch driver (CPU baseline): force_distribution + force_opt for n robots,
+ * row layout of qloco_force_qp_solve; states = n initialised records */
+void qo_force_batch(int64_t n, qo_dyn_state *states, const qo_force_params *prm,
+                    const double *com_des, const double *leg_des, const double *F_force_des,
+                    const double *rfoot_des, const double *lfoot_des, const double *base_p,
+                    const double *feet_p, const double *FT_total_des, const int32_t *mode,
+                    const int32_t *right_support, const double *y_coef, double *grf_opt);
 /* dynmics_compute.cpp:109-138; Jaco 3x3 col-major; swing_flag = `support_flag` */
 void qo_compute_joint_torques(const qo_dyn_state *s, const double Jaco[9],
                               int swing_flag, const double p_des[3],

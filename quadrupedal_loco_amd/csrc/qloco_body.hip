@@ -13,6 +13,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "qloco_gi_core.hpp"
 
 namespace qloco {
@@ -131,13 +133,24 @@ struct BodyArgs {
   const double *tx;
   int64_t tx_stride;
   const int32_t *run;
+  // row stride (doubles) of the reference arrays: 0 = packed (4 / 10 / 15);
+  // the rt tick keeps all of a robot's references in one 64-double record
+  int64_t ref_ld;
 };
 
+// constant inequality rows (:541-561, :805-812): CI(:, c) = -[q_upx' q_lowx'
+// q_upy' q_lowy' t_upx' t_lowx' t_upy' t_lowy'], columns 32..47 zero.  The
+// same for every robot, so it lives in constant memory (set once per device)
+// rather than in each workgroup's LDS.
+__constant__ double c_body_CI[BNT * BNI];
+// The Initialize() constants, also in constant memory: as a by-value kernel
+// argument the dynamically indexed struct was materialised in VGPRs.
+__constant__ BodyConsts c_body_K;
+
 struct BodyLds {
-  double CI[BNT * BNI];
   struct Grp {
     double G[BNT * BNT], g0[BNT], ci0[BNI], x[16];
-    GiLds gi;
+    GiLdsT<BNT, BNI, 0> gi;
   } g[GI_GROUPS];
 };
 
@@ -157,36 +170,20 @@ __device__ __forceinline__ int indexfind(const double *tx, int64_t stride, doubl
 #define R2(m, r, c) ((m)[(c)*2 + (r)])
 #define R3(m, r, c) ((m)[(c)*3 + (r)])
 
-__global__ __launch_bounds__(64) void body_mpc_kernel(const BodyArgs a) {
+// 2 waves/SIMD: the LDS (19 KB per 4-robot block) admits 8 blocks per CU; the
+// register budget is set to match (160 VGPRs, no spills)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void body_mpc_kernel(const BodyArgs a) {
   __shared__ BodyLds S;
-  const BodyConsts &K = a.k;
+  const BodyConsts &K = c_body_K;
   const int lane = threadIdx.x, grp = lane >> 4, li = lane & 15;
   const int64_t inst = (int64_t)blockIdx.x * GI_GROUPS + grp;
-  // constant rows (:541-561, :805-812): CI(:, c) = -[q_upx' q_lowx' q_upy'
-  // q_lowy' t_upx' t_lowx' t_upy' t_lowy'], columns 32..47 zero
-  for (int t = lane; t < BNT * BNI; t += 64) S.CI[t] = 0.0;
-  __syncthreads();
-  if (lane < BNH) {
-    const int row = lane;
-    for (int v = 0; v < BNH; ++v) {
-      const double pu = K.ppu[v * BNH + row];
-      S.CI[(0 * BNH + row) * BNT + v] = -pu;
-      S.CI[(1 * BNH + row) * BNT + v] = pu;
-      S.CI[(2 * BNH + row) * BNT + BNH + v] = -pu;
-      S.CI[(3 * BNH + row) * BNT + BNH + v] = pu;
-    }
-    S.CI[(4 * BNH + row) * BNT + row] = -K.j_ini;
-    S.CI[(5 * BNH + row) * BNT + row] = K.j_ini;
-    S.CI[(6 * BNH + row) * BNT + BNH + row] = -K.j_ini;
-    S.CI[(7 * BNH + row) * BNT + BNH + row] = K.j_ini;
-  }
-  __syncthreads();
   if (inst >= a.batch) return;
   BodyLds::Grp &P = S.g[grp];
   double *st = a.state + inst * QLOCO_BODY_STATE_LEN;
-  const double *zmp_ref = a.zmp_ref + inst * 10, *angle_ref = a.angle_ref + inst * 10;
-  const double *rfoot_ref = a.rfoot_ref + inst * 10, *lfoot_ref = a.lfoot_ref + inst * 10;
-  const double *comacc_ref = a.comacc_ref + inst * 15;
+  const int64_t l10 = a.ref_ld ? a.ref_ld : 10, l15 = a.ref_ld ? a.ref_ld : 15;
+  const double *zmp_ref = a.zmp_ref + inst * l10, *angle_ref = a.angle_ref + inst * l10;
+  const double *rfoot_ref = a.rfoot_ref + inst * l10, *lfoot_ref = a.lfoot_ref + inst * l10;
+  const double *comacc_ref = a.comacc_ref + inst * l15;
   double thetaxk[2] = {st[0], st[1]}, thetayk[2] = {st[2], st[3]};
   int i = a.i[inst];
   int status = QLOCO_OK;
@@ -283,7 +280,7 @@ __global__ __launch_bounds__(64) void body_mpc_kernel(const BodyArgs a) {
     GI_SYNC();
     double f;
     int it;
-    gi_solve_group(P.gi, li, BNT, 0, BNI, P.G, BNT, P.g0, nullptr, nullptr, S.CI, P.ci0, P.x, f,
+    gi_solve_group(P.gi, li, BNT, 0, BNI, P.G, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
                    status, it);
     GI_SYNC();
     if (li == 0) {
@@ -334,7 +331,7 @@ __global__ __launch_bounds__(64) void body_mpc_kernel(const BodyArgs a) {
       thetaxk[1] = txk_tmp[1];
       thetayk[0] = tyk_tmp[0];
       thetayk[1] = tyk_tmp[1];
-      const double *bs = a.bodyangle_state + inst * 4;  // lambda feedback, all 0 (:664-692)
+      const double *bs = a.bodyangle_state + inst * (a.ref_ld ? a.ref_ld : 4);  // lambda feedback, all 0 (:664-692)
       const double lx = 0.0, lvx = 0.0, ly = 0.0, lvy = 0.0;
       thetaxk[0] = lx * bs[0] + (1 - lx) * thetaxk[0];
       thetaxk[1] = lvx * bs[1] + (1 - lvx) * thetaxk[1];
@@ -364,7 +361,7 @@ int body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyangle_sta
                     const double *zmp_ref, const double *angle_ref, const double *rfoot_ref,
                     const double *lfoot_ref, const double *comacc_ref, double *state,
                     double *com_traj, int32_t *status, const double *tx, int64_t tx_stride,
-                    const int32_t *run, hipStream_t stream);
+                    const int32_t *run, int64_t ref_ld, hipStream_t stream);
 
 __global__ void indexfind_kernel(const BodyConsts k, int64_t batch, const double *t, int *j) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -394,8 +391,37 @@ extern "C" int qloco_body_mpc_step(int64_t batch, const int32_t *i,
       !comacc_ref || !state || !com_traj)
     return QLOCO_ERR_ARG;
   return body_mpc_launch(batch, i, bodyangle_state, zmp_ref, angle_ref, rfoot_ref, lfoot_ref,
-                         comacc_ref, state, com_traj, status, nullptr, 0, nullptr,
+                         comacc_ref, state, com_traj, status, nullptr, 0, nullptr, 0,
                          (hipStream_t)stream);
+}
+
+// c_body_CI / c_body_K from the Initialize() constants, once per device
+static int body_ci_upload(const BodyConsts &K) {
+  static std::mutex mu;
+  static bool done[256] = {};
+  int dev = 0;
+  QLOCO_HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
+  std::lock_guard<std::mutex> lock(mu);
+  if (dev >= 0 && dev < 256 && done[dev]) return QLOCO_OK;
+  double CI[BNT * BNI];
+  memset(CI, 0, sizeof(CI));
+  for (int row = 0; row < BNH; ++row) {
+    for (int v = 0; v < BNH; ++v) {
+      const double pu = K.ppu[v * BNH + row];
+      CI[(0 * BNH + row) * BNT + v] = -pu;
+      CI[(1 * BNH + row) * BNT + v] = pu;
+      CI[(2 * BNH + row) * BNT + BNH + v] = -pu;
+      CI[(3 * BNH + row) * BNT + BNH + v] = pu;
+    }
+    CI[(4 * BNH + row) * BNT + row] = -K.j_ini;
+    CI[(5 * BNH + row) * BNT + row] = K.j_ini;
+    CI[(6 * BNH + row) * BNT + BNH + row] = -K.j_ini;
+    CI[(7 * BNH + row) * BNT + BNH + row] = K.j_ini;
+  }
+  QLOCO_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_body_CI), CI, sizeof(CI)), "c_body_CI upload");
+  QLOCO_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_body_K), &K, sizeof(K)), "c_body_K upload");
+  if (dev >= 0 && dev < 256) done[dev] = true;
+  return QLOCO_OK;
 }
 
 int qloco::body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyangle_state,
@@ -403,7 +429,7 @@ int qloco::body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyan
                            const double *rfoot_ref, const double *lfoot_ref,
                            const double *comacc_ref, double *state, double *com_traj,
                            int32_t *status, const double *tx, int64_t tx_stride,
-                           const int32_t *run, hipStream_t stream) {
+                           const int32_t *run, int64_t ref_ld, hipStream_t stream) {
   BodyArgs a;
   memset(&a, 0, sizeof(a));
   body_constants(a.k);
@@ -421,6 +447,9 @@ int qloco::body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyan
   a.tx = tx;
   a.tx_stride = tx_stride;
   a.run = run;
+  a.ref_ld = ref_ld;
+  const int rc = body_ci_upload(a.k);
+  if (rc != QLOCO_OK) return rc;
   const unsigned blocks = (unsigned)((batch + GI_GROUPS - 1) / GI_GROUPS);
   hipLaunchKernelGGL(body_mpc_kernel, dim3(blocks), dim3(64), 0, stream, a);
   QLOCO_HIP_CHECK(hipGetLastError(), "body_mpc_kernel launch");

@@ -31,7 +31,7 @@ struct ForceLds {
   double zeros[16];
   struct Grp {
     double G[144], g0[12], CE[144], A[72], x[16], guess[12];
-    GiLds gi;
+    GiLdsT<12, 24, 12> gi;
   } g[GI_GROUPS];
 };
 

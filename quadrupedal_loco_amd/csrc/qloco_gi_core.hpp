@@ -16,14 +16,20 @@ constexpr int GI_M = 64;                 // max inequalities
 constexpr int GI_PM = GI_P + GI_M + 1;
 constexpr int GI_GROUPS = 4;             // instances per wavefront
 
-struct GiLds {
-  double J[GI_N * GI_N];  // col-major, J(r,c) = J[c*GI_N + r]
-  double R[GI_N * GI_N];
-  double x[GI_N], z[GI_N], d[GI_N], np[GI_N], xold[GI_N];
-  double s[GI_M];
-  double r[GI_PM], u[GI_PM], uold[GI_PM];
-  int A[GI_PM], Aold[GI_PM], iai[GI_PM], iaexcl[GI_PM];
+// Per-group LDS work space, sized for at most NN variables, MM inequalities
+// and PP equalities (the generic kernel uses the GI_* limits; the force and
+// body kernels instantiate their exact sizes so more groups fit per CU).
+template <int NN, int MM, int PP>
+struct GiLdsT {
+  static constexpr int PMM = PP + MM + 1;
+  double J[NN * NN];  // col-major, J(r,c) = J[c*NN + r]
+  double R[NN * NN];
+  double x[NN], z[NN], d[NN], np[NN], xold[NN];
+  double s[MM];
+  double r[PMM], u[PMM], uold[PMM];
+  int A[PMM], Aold[PMM], iai[PMM], iaexcl[PMM];
 };
+using GiLds = GiLdsT<GI_N, GI_M, GI_P>;
 
 struct GiArgs {
   int n, p, m;
@@ -51,14 +57,15 @@ __device__ __forceinline__ double gi_distance(double a, double b) {  // EiQuadPr
 }
 
 // One group's view of the problem.
+template <int NN, int MM, int PP>
 struct GiGroup {
-  GiLds *L;
+  GiLdsT<NN, MM, PP> *L;
   int li;  // lane in group (0..15)
   int n, p, m;
   const double *CE, *ce0, *CI, *ci0;
-  __device__ __forceinline__ double J(int r, int c) const { return L->J[c * GI_N + r]; }
-  __device__ __forceinline__ double &Jr(int r, int c) { return L->J[c * GI_N + r]; }
-  __device__ __forceinline__ double &Rr(int r, int c) { return L->R[c * GI_N + r]; }
+  __device__ __forceinline__ double J(int r, int c) const { return L->J[c * NN + r]; }
+  __device__ __forceinline__ double &Jr(int r, int c) { return L->J[c * NN + r]; }
+  __device__ __forceinline__ double &Rr(int r, int c) { return L->R[c * NN + r]; }
   __device__ __forceinline__ double CEc(int r, int i) const { return CE[(int64_t)i * n + r]; }
   __device__ __forceinline__ double CIc(int r, int i) const { return CI[(int64_t)i * n + r]; }
 
@@ -86,9 +93,9 @@ struct GiGroup {
   __device__ __forceinline__ void update_r(int iq) {
     for (int i = iq - 1; i >= 0; --i) {
       double acc = L->d[i];
-      for (int j = i + 1; j < iq; ++j) acc -= L->R[j * GI_N + i] * L->r[j];
+      for (int j = i + 1; j < iq; ++j) acc -= L->R[j * NN + i] * L->r[j];
       GI_SYNC();
-      if (li == 0) L->r[i] = acc / L->R[i * GI_N + i];
+      if (li == 0) L->r[i] = acc / L->R[i * NN + i];
       GI_SYNC();
     }
   }
@@ -148,7 +155,7 @@ struct GiGroup {
         L->A[i] = L->A[i + 1];
         L->u[i] = L->u[i + 1];
       }
-      if (li < n) Rr(li, i) = L->R[(i + 1) * GI_N + li];
+      if (li < n) Rr(li, i) = L->R[(i + 1) * NN + li];
       GI_SYNC();
     }
     GI_SYNC();
@@ -163,8 +170,8 @@ struct GiGroup {
     iq--;
     if (iq == 0) return true;
     for (int j = qq; j < iq; j++) {
-      double cc = L->R[j * GI_N + j];
-      double ss = L->R[j * GI_N + j + 1];
+      double cc = L->R[j * NN + j];
+      double ss = L->R[j * NN + j + 1];
       const double h = gi_distance(cc, ss);
       if (h == 0.0) continue;
       cc = cc / h;
@@ -187,8 +194,8 @@ struct GiGroup {
       {
         const int k = li;
         if (k >= j + 1 && k < iq) {
-          const double t1 = L->R[k * GI_N + j];
-          const double t2 = L->R[k * GI_N + j + 1];
+          const double t1 = L->R[k * NN + j];
+          const double t2 = L->R[k * NN + j + 1];
           const double nj = t1 * cc + t2 * ss;
           Rr(j, k) = nj;
           Rr(j + 1, k) = xny * (t1 + nj) - t2;
@@ -214,11 +221,12 @@ struct GiGroup {
 // Solve one QP with the 16 lanes of a group.  G (n x n, ld = ldG), g0, CE
 // (n x p), ce0, CI (n x m), ci0 may live in global memory or LDS (flat
 // pointers).  Writes x (n) to xout (lane li < n writes element li).
-__device__ __noinline__ void gi_solve_group(GiLds &S, int li, int n, int p, int m, const double *G, int ldG,
+template <int NN, int MM, int PP>
+__device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, int n, int p, int m, const double *G, int ldG,
                                const double *g0, const double *CE, const double *ce0,
                                const double *CI, const double *ci0, double *xout,
                                double &f_out, int &status_out, int &iters_out) {
-  GiGroup g;
+  GiGroup<NN, MM, PP> g;
   g.L = &S;
   g.li = li;
   g.n = n;
@@ -233,7 +241,7 @@ __device__ __noinline__ void gi_solve_group(GiLds &S, int li, int n, int p, int 
   int iter = 0;
   double f_value = 0.0;
   // persistent-member semantics: start every solve from zeroed index arrays
-  for (int k = li; k < GI_PM; k += 16) {
+  for (int k = li; k < (PP + MM + 1); k += 16) {
     S.A[k] = 0;
     S.Aold[k] = 0;
     S.iai[k] = 0;
@@ -246,15 +254,15 @@ __device__ __noinline__ void gi_solve_group(GiLds &S, int li, int n, int p, int 
   double c1 = 0.0;
   for (int i = 0; i < n; ++i) c1 += G[i * ldG + i];
   // L is built in R (zeroed again before solve_quadprog2 uses R)
-  for (int k = li; k < GI_N * GI_N; k += 16) S.R[k] = 0.0;
+  for (int k = li; k < NN * NN; k += 16) S.R[k] = 0.0;
   GI_SYNC();
   if (li < n)
-    for (int c = 0; c <= li; ++c) S.R[c * GI_N + li] = G[c * ldG + li];  // lower triangle, row li
+    for (int c = 0; c <= li; ++c) S.R[c * NN + li] = G[c * ldG + li];  // lower triangle, row li
   GI_SYNC();
   bool pd = true;
   for (int k = 0; k < n; ++k) {
-    double x = S.R[k * GI_N + k];
-    for (int j = 0; j < k; ++j) x -= S.R[j * GI_N + k] * S.R[j * GI_N + k];
+    double x = S.R[k * NN + k];
+    for (int j = 0; j < k; ++j) x -= S.R[j * NN + k] * S.R[j * NN + k];
     if (!(x > 0.0)) {
       pd = false;
       break;
@@ -263,13 +271,13 @@ __device__ __noinline__ void gi_solve_group(GiLds &S, int li, int n, int p, int 
     const int r = li;
     double lrk = 0.0;
     if (r > k && r < n) {
-      double acc = S.R[k * GI_N + r];
-      for (int j = 0; j < k; ++j) acc -= S.R[j * GI_N + r] * S.R[j * GI_N + k];
+      double acc = S.R[k * NN + r];
+      for (int j = 0; j < k; ++j) acc -= S.R[j * NN + r] * S.R[j * NN + k];
       lrk = acc / lkk;
     }
     GI_SYNC();
-    if (r > k && r < n) S.R[k * GI_N + r] = lrk;
-    if (li == 0) S.R[k * GI_N + k] = lkk;
+    if (r > k && r < n) S.R[k * NN + r] = lrk;
+    if (li == 0) S.R[k * NN + k] = lkk;
     GI_SYNC();
   }
   if (!pd) {
@@ -283,24 +291,24 @@ __device__ __noinline__ void gi_solve_group(GiLds &S, int li, int n, int p, int 
       const int c = li;
       for (int rr = n - 1; rr >= 0; --rr) {
         double acc = (rr == c) ? 1.0 : 0.0;
-        for (int j = rr + 1; j < n; ++j) acc -= S.R[rr * GI_N + j] * S.J[c * GI_N + j];
-        S.J[c * GI_N + rr] = acc / S.R[rr * GI_N + rr];
+        for (int j = rr + 1; j < n; ++j) acc -= S.R[rr * NN + j] * S.J[c * NN + j];
+        S.J[c * NN + rr] = acc / S.R[rr * NN + rr];
       }
     }
     GI_SYNC();
     double c2 = 0.0;
-    for (int i = 0; i < n; ++i) c2 += S.J[i * GI_N + i];
+    for (int i = 0; i < n; ++i) c2 += S.J[i * NN + i];
     // x = -G^-1 g0 through the factor (:227-230), serial, lane 0
     if (li == 0) {
       for (int i = 0; i < n; ++i) {
         double acc = g0[i];
-        for (int j = 0; j < i; ++j) acc -= S.R[j * GI_N + i] * S.x[j];
-        S.x[i] = acc / S.R[i * GI_N + i];
+        for (int j = 0; j < i; ++j) acc -= S.R[j * NN + i] * S.x[j];
+        S.x[i] = acc / S.R[i * NN + i];
       }
       for (int i = n - 1; i >= 0; --i) {
         double acc = S.x[i];
-        for (int j = i + 1; j < n; ++j) acc -= S.R[i * GI_N + j] * S.x[j];
-        S.x[i] = acc / S.R[i * GI_N + i];
+        for (int j = i + 1; j < n; ++j) acc -= S.R[i * NN + j] * S.x[j];
+        S.x[i] = acc / S.R[i * NN + i];
       }
       for (int i = 0; i < n; ++i) S.x[i] = -S.x[i];
     }
@@ -309,8 +317,8 @@ __device__ __noinline__ void gi_solve_group(GiLds &S, int li, int n, int p, int 
     for (int i = 0; i < n; ++i) f_value += g0[i] * S.x[i];
     f_value *= 0.5;
     // solve_quadprog2 preprocessing: d = 0, R = 0, R_norm = 1 (:207-209)
-    for (int k = li; k < GI_N * GI_N; k += 16) S.R[k] = 0.0;
-    if (li < GI_N) S.d[li] = 0.0;
+    for (int k = li; k < NN * NN; k += 16) S.R[k] = 0.0;
+    if (li < NN) S.d[li] = 0.0;
     GI_SYNC();
     double R_norm = 1.0;
     const int me = p, mi = m;

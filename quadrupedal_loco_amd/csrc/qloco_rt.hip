@@ -42,7 +42,7 @@ int body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyangle_sta
                     const double *zmp_ref, const double *angle_ref, const double *rfoot_ref,
                     const double *lfoot_ref, const double *comacc_ref, double *state,
                     double *com_traj, int32_t *status, const double *tx, int64_t tx_stride,
-                    const int32_t *run, hipStream_t stream);
+                    const int32_t *run, int64_t ref_ld, hipStream_t stream);
 
 namespace rt {
 
@@ -81,8 +81,13 @@ enum : int {
 enum : int { I_LOOP = 0, I_MPC, I_INT, I_TINT, I_FLAGOLD, I_TEND, I_BJXX, I_INTS };
 enum { RX = 0, RY, RZ, RVX, RVY, RVZ, RAX, RAY, RAZ, LX, LY, LZ, LVX, LVY, LVZ, LAX, LAY, LAZ };
 
+// body_theta_mpc reference record per robot (doubles): bodyangle_state,
+// zmp_mpc_ref, bodyangle_mpc_ref, rfoot_mpc_ref, lfoot_mpc_ref (Eigen 2x5
+// col-major), comacc_mpc_ref (3x5)
+enum : int { RF_BAS = 0, RF_ZMP = 4, RF_ANG = 14, RF_RFT = 24, RF_LFT = 34, RF_ACC = 44,
+             RF_USED = 59, RF_LD = 64 };
 struct Ws {  // byte offsets into the workspace
-  int64_t d, n, body, zmp, ang, rft, lft, acc, bas, ct, bi, run, st, total;
+  int64_t d, n, body, ref, ct, bi, run, st, total;
 };
 __host__ __device__ inline Ws layout(int64_t B) {
   Ws w;
@@ -90,13 +95,8 @@ __host__ __device__ inline Ws layout(int64_t B) {
   w.d = 0;
   w.n = al(w.d + 8 * F_DOUBLES * B);
   w.body = al(w.n + 4 * I_INTS * B);
-  w.zmp = al(w.body + 8 * QLOCO_BODY_STATE_LEN * B);
-  w.ang = al(w.zmp + 8 * 10 * B);
-  w.rft = al(w.ang + 8 * 10 * B);
-  w.lft = al(w.rft + 8 * 10 * B);
-  w.acc = al(w.lft + 8 * 10 * B);
-  w.bas = al(w.acc + 8 * 15 * B);
-  w.ct = al(w.bas + 8 * 4 * B);
+  w.ref = al(w.body + 8 * QLOCO_BODY_STATE_LEN * B);
+  w.ct = al(w.ref + 8 * RF_LD * B);
   w.bi = al(w.ct + 8 * 14 * B);
   w.run = al(w.bi + 4 * B);
   w.st = al(w.run + 4 * B);
@@ -115,8 +115,8 @@ struct RtArgs {
 
 // per-lane view of one robot's SoA state
 struct Robot {
-  double *d;
-  int32_t *n;
+  double *__restrict__ d;
+  int32_t *__restrict__ n;
   int64_t B;
   __device__ double &D(int f) const { return d[(int64_t)f * B]; }
   __device__ int32_t &I(int f) const { return n[(int64_t)f * B]; }
@@ -130,6 +130,17 @@ __device__ __forceinline__ int indexfind(const Robot &R, double goal) {
   while (j < NS && goal >= R.D(F_TX + j)) j++;
   return j - 1;
 }
+// The same scan for a non-decreasing sequence of goals: _tx is non-decreasing
+// (every _ts > 0, and round(tx/dt)*dt - 1e-5 never decreases), so every
+// j < the previous answer + 1 still satisfies goal >= _tx(j) and the scan may
+// resume there -- the result equals the reference's scan from 0.
+struct IndexScan {
+  int j = 0;
+  __device__ __forceinline__ int operator()(const Robot &R, double goal) {
+    while (j < NS && goal >= R.D(F_TX + j)) j++;
+    return j - 1;
+  }
+};
 
 // std::pow(t, 3) / pow(t, 2) as in oracle/rt_tick.c: compensated cube (fma
 // error-free products, one final rounding), exact-rounded square
@@ -143,31 +154,51 @@ __host__ __device__ inline double cube(double x) {
 // Dense 4x4 inverse, Gauss-Jordan with partial pivoting (row-major), the
 // same algorithm and operation order as oracle/rt_tick.c:qo_inv4
 __host__ __device__ inline void inv4(const double A[16], double Ai[16]) {
+  // every index static (pivot search by value, row swap by selects), so the
+  // 4x8 tableau stays in registers
   double M[4][8];
+#pragma unroll
   for (int r = 0; r < 4; ++r)
+#pragma unroll
     for (int c = 0; c < 4; ++c) {
       M[r][c] = A[r * 4 + c];
       M[r][4 + c] = (r == c) ? 1.0 : 0.0;
     }
+#pragma unroll
   for (int k = 0; k < 4; ++k) {
     int p = k;
-    for (int r = k + 1; r < 4; ++r)
-      if (fabs(M[r][k]) > fabs(M[p][k])) p = r;
-    if (p != k)
-      for (int c = 0; c < 8; ++c) {
-        const double t = M[k][c];
-        M[k][c] = M[p][c];
-        M[p][c] = t;
+    double best = fabs(M[k][k]);
+#pragma unroll
+    for (int r = k + 1; r < 4; ++r) {
+      const double v = fabs(M[r][k]);
+      if (v > best) {
+        best = v;
+        p = r;
       }
+    }
+#pragma unroll
+    for (int r = k + 1; r < 4; ++r)
+      if (p == r)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const double t = M[k][c];
+          M[k][c] = M[r][c];
+          M[r][c] = t;
+        }
     const double piv = M[k][k];
+#pragma unroll
     for (int c = 0; c < 8; ++c) M[k][c] = M[k][c] / piv;
+#pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (r == k) continue;
       const double f = M[r][k];
+#pragma unroll
       for (int c = 0; c < 8; ++c) M[r][c] = M[r][c] - f * M[k][c];
     }
   }
+#pragma unroll
   for (int r = 0; r < 4; ++r)
+#pragma unroll
     for (int c = 0; c < 4; ++c) Ai[r * 4 + c] = M[r][4 + c];
 }
 
@@ -253,7 +284,7 @@ __device__ __forceinline__ void swing_axis(const Robot &R, const double Ai[16], 
 
 // Foot_trajectory_solve_mod2 (PRMPCClass.cpp:1756-2195), _stopwalking = false
 __device__ void foot_traj_mod2(const Robot &R, int j_indexx, const double nrt[9], int &bjx1,
-                               int &bjxx, int &t_end) {
+                               int &bjxx, int &t_end, int sched_xx[NH], int sched_x1[NH]) {
   const int bjxx_nrt = (int)nrt[0];
   if (bjxx_nrt >= 0 && bjxx_nrt + 1 < NS) {  // :1758-1764 (unchecked in the reference)
     R.fxyz(0, bjxx_nrt) = nrt[1];
@@ -268,13 +299,16 @@ __device__ void foot_traj_mod2(const Robot &R, int j_indexx, const double nrt[9]
   recompute_tx(R);
   t_end = (int)round((R.D(F_TX + NS - 1) - 2 * TSTEP) / DT_FAST);  // :1780
   R.D(F_TXTOT) = R.D(F_TX + NS - 1);
+  IndexScan scan;  // goals j*dt, (j+1)*dt, (j+1)*dt, ... never decrease
 #pragma unroll
   for (int kk = 1; kk <= NH; ++kk) {
     const int j_index = j_indexx + kk - 1, k = kk;
     if (j_index <= t_end) {  // :1790-1799
-      bjxx = indexfind(R, j_index * DT_FAST) + 1;
-      bjx1 = indexfind(R, (j_index + 1) * DT_FAST) + 1;
+      bjxx = scan(R, j_index * DT_FAST) + 1;
+      bjx1 = scan(R, (j_index + 1) * DT_FAST) + 1;
     }
+    sched_xx[kk - 1] = bjxx;
+    sched_x1[kk - 1] = bjx1;
     if (j_index > t_end)  // :1801-1807
       for (int i_t = bjx1 + 1; i_t < NS; i_t++) R.D(F_LIFT + i_t) = 0;
     for (int i_t = 24; i_t < NS; i_t++) R.D(F_LIFT + i_t) = 0;  // :1809-1811
@@ -352,13 +386,16 @@ __device__ void foot_traj_mod2(const Robot &R, int j_indexx, const double nrt[9]
 }
 
 // XGetSolution_Foot_rotation (PRMPCClass.cpp:2255-2380)
-__device__ void foot_rotation(const Robot &R, int walktimex, int &bjx1, int &bjxx, int t_end) {
+// the Indexfind calls here repeat Foot_trajectory_solve_mod2's (same goals,
+// same _tx, same _t_end_footstep test), so their results are reused
+__device__ void foot_rotation(const Robot &R, int walktimex, int &bjx1, int &bjxx, int t_end,
+                              const int sched_xx[NH], const int sched_x1[NH]) {
 #pragma unroll
   for (int c = 0; c < NH; ++c) {
     const int walktime = walktimex + c;
     if (walktime <= t_end) {
-      bjxx = indexfind(R, walktime * DT_FAST) + 1;
-      bjx1 = indexfind(R, (walktime + 1) * DT_FAST) + 1;
+      bjxx = sched_xx[c];
+      bjx1 = sched_x1[c];
     }
     const int b1 = bjx1;
     if ((b1 >= 2) && (walktime <= t_end)) {
@@ -452,143 +489,184 @@ __device__ void interpolation(const RtArgs &a, const Robot &R, const double *g, 
   R.I(I_INT) = cnt;
 }
 
-__global__ __launch_bounds__(256) void rt_pre_kernel(const RtArgs a) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t B = a.B;
-  if (r >= B) return;
-  const Ws L = layout(B);
-  Robot R{reinterpret_cast<double *>(a.ws + L.d) + r, reinterpret_cast<int32_t *>(a.ws + L.n) + r, B};
-  double *body = reinterpret_cast<double *>(a.ws + L.body) + r * QLOCO_BODY_STATE_LEN;
-  int32_t *run = reinterpret_cast<int32_t *>(a.ws + L.run) + r;
-  int32_t *bi = reinterpret_cast<int32_t *>(a.ws + L.bi) + r;
-  const double *g = a.gait + r * QLOCO_GAIT_MSG_LEN;
-  const double *ctrl = a.ctrl + r * QLOCO_CTRL_MSG_LEN;
-  // callbacks (:79-110)
-  const int flag = (int)g[99];
-  double nrt[9];
-  for (int k = 0; k < 9; ++k) nrt[k] = g[86 + k];
-  double *bas = reinterpret_cast<double *>(a.ws + L.bas) + r * 4;
-  bas[0] = ctrl[10];
-  bas[1] = ctrl[11];
-  bas[2] = ctrl[13];
-  bas[3] = ctrl[14];
-  int do_body = 0;
-  if (ctrl[0] > 0) {
-    const int loop = R.I(I_LOOP) + 1;
-    R.I(I_LOOP) = loop;
-    const int t_int = (int)((uint32_t)R.I(I_TINT) + (uint32_t)(int)floor((double)(loop / 2)));
-    R.I(I_TINT) = t_int;
-    R.D(F_NRT + 0) = t_int;  // state_to_MPC = state_feedback (:519-527)
-    for (int k = 1; k < 25; ++k) R.D(F_NRT + k) = ctrl[k];
-    if (flag > 0) {
-      const int mpc = R.I(I_MPC) + 1;
-      R.I(I_MPC) = mpc;
-      int t_end = R.I(I_TEND);
-      interpolation(a, R, g, flag, t_int, t_end);
-      if (mpc * DT_FAST > 1.0) {  // _height_offset_timex = 1 (:537-545)
-        const int foot_i = (int)(mpc - (int)1.0 / DT_FAST);
-        int bjx1 = (int)body[26], bjxx = R.I(I_BJXX);
-        foot_traj_mod2(R, foot_i, nrt, bjx1, bjxx, t_end);
-        foot_rotation(R, foot_i, bjx1, bjxx, t_end);
-        body[26] = bjx1;
-        R.I(I_BJXX) = bjxx;
-        R.I(I_TEND) = t_end;
-      }
-      R.D(F_ZMP + 8) = 0.0;  // zmpxyz_ref(2) = _Zsc = {l,r}foot_inter(2) = 0 (:557-566)
-      // body_theta_mpc references (:568-616), Eigen col-major 2x5 / 3x5
-      double *zmp = reinterpret_cast<double *>(a.ws + L.zmp) + r * 10;
-      double *ang = reinterpret_cast<double *>(a.ws + L.ang) + r * 10;
-      double *rft = reinterpret_cast<double *>(a.ws + L.rft) + r * 10;
-      double *lft = reinterpret_cast<double *>(a.ws + L.lft) + r * 10;
-      double *acc = reinterpret_cast<double *>(a.ws + L.acc) + r * 15;
-      for (int j = 0; j < 5; ++j) {
-        if (j == 0) {
-          zmp[0] = R.D(F_ZINT + 0);
-          zmp[1] = R.D(F_ZINT + 1);
-        } else {
-          zmp[2 * j] = R.D(F_ZINT + 8 + 3 * j - 2);
-          zmp[2 * j + 1] = R.D(F_ZINT + 8 + 3 * j - 1);
-        }
-        rft[2 * j] = R.D(F_FOORPR + j * 6 + 1);  // row 0 assigned twice, x then y
-        rft[2 * j + 1] = 0.0;                    // row 1 never assigned
-        lft[2 * j] = R.D(F_FOORPR + j * 6 + 3);
-        lft[2 * j + 1] = R.D(F_FOORPR + j * 6 + 4);
-        ang[2 * j] = (R.D(F_FTHETA + j * 6) + R.D(F_FTHETA + j * 6 + 3)) / 5;
-        ang[2 * j + 1] = (R.D(F_FTHETA + j * 6 + 1) + R.D(F_FTHETA + j * 6 + 4)) / 5;
-        acc[3 * j] = 0.0;
-        acc[3 * j + 1] = 0.0;
-        acc[3 * j + 2] = (j == 0) ? R.D(F_CACC + 2) : R.D(F_CACC + 8 + 3 * j);
-      }
-      R.D(F_BTHX + 0) = ang[0];
-      R.D(F_BTHX + 1) = ang[1];
-      *bi = mpc;
-      do_body = 1;
-    }
+// body_theta_mpc reference record slot k (RF_* layout) of robot R, from the
+// generator outputs (gait_fast.cpp:568-616): zmp from zmp_inter, rfoot row 0
+// = the y entry (assigned twice, :585-586) and row 1 never set, lfoot x/y,
+// body angle = (right + left foot rotation) / 5, comacc row 2 only
+__device__ __forceinline__ double ref_slot(const Robot &R, const double *ctrl, int k) {
+  if (k < RF_ZMP) return ctrl[k < 2 ? 10 + k : 11 + k];  // state_feedback(10, 11, 13, 14)
+  if (k < RF_ANG) {
+    const int e = k - RF_ZMP, j = e >> 1, rr = e & 1;
+    return j == 0 ? R.D(F_ZINT + rr) : R.D(F_ZINT + 8 + 3 * j - 2 + rr);
   }
-  *run = do_body;
+  if (k < RF_RFT) {
+    const int e = k - RF_ANG, j = e >> 1, rr = e & 1;
+    return (R.D(F_FTHETA + j * 6 + rr) + R.D(F_FTHETA + j * 6 + 3 + rr)) / 5;
+  }
+  if (k < RF_LFT) {
+    const int e = k - RF_RFT, j = e >> 1, rr = e & 1;
+    return rr == 0 ? R.D(F_FOORPR + j * 6 + 1) : 0.0;
+  }
+  if (k < RF_ACC) {
+    const int e = k - RF_LFT, j = e >> 1, rr = e & 1;
+    return R.D(F_FOORPR + j * 6 + 3 + rr);
+  }
+  const int e = k - RF_ACC, j = e / 3, rr = e - 3 * j;
+  if (rr != 2) return 0.0;
+  return j == 0 ? R.D(F_CACC + 2) : R.D(F_CACC + 8 + 3 * j);
 }
 
-__global__ __launch_bounds__(256) void rt_post_kernel(const RtArgs a) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t B = a.B;
-  if (r >= B) return;
+constexpr int PRE_T = 256;   // robots per block
+constexpr int STG_C = 16;    // slots per transpose chunk
+constexpr int STG_LD = 17;   // LDS row stride (doubles): odd, conflict-free column reads
+
+// Stage `count` slots of every robot of the block (value(k) for k < count)
+// through LDS and store them to out[(r0 + robot) * ld + off + k], so that
+// consecutive lanes write consecutive doubles of a row (a per-lane row store
+// touches 64 cache lines per instruction, the staged one 2-3).
+template <int T, typename F>
+__device__ __forceinline__ void stage_rows(double *stage, int tid, int nb, int64_t r0, bool live,
+                                           int count, double *out, int ld, int off, F value) {
+#pragma unroll
+  for (int c0 = 0; c0 < count; c0 += STG_C) {
+    const int w = (count - c0) < STG_C ? (count - c0) : STG_C;
+    if (live)
+#pragma unroll
+      for (int j = 0; j < STG_C; ++j)
+        if (j < w) stage[tid * STG_LD + j] = value(c0 + j);
+    __syncthreads();
+    for (int idx = tid; idx < nb * w; idx += T) {
+      const int rr = idx / w, j = idx - rr * w;
+      out[(r0 + rr) * ld + off + c0 + j] = stage[rr * STG_LD + j];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(PRE_T) void rt_pre_kernel(const RtArgs a) {
+  __shared__ double stage[PRE_T * STG_LD];
+  const int tid = threadIdx.x;
+  const int64_t B = a.B, r0 = (int64_t)blockIdx.x * PRE_T;
+  const int nb = (int)((B - r0) < PRE_T ? (B - r0) : PRE_T);
+  const int64_t r = r0 + tid;
+  const bool live = tid < nb;
+  const Ws L = layout(B);
+  Robot R{reinterpret_cast<double *>(a.ws + L.d) + r, reinterpret_cast<int32_t *>(a.ws + L.n) + r, B};
+  const double *ctrl = a.ctrl + r * QLOCO_CTRL_MSG_LEN;
+  int do_body = 0;
+  if (live) {
+    double *body = reinterpret_cast<double *>(a.ws + L.body) + r * QLOCO_BODY_STATE_LEN;
+    int32_t *bi = reinterpret_cast<int32_t *>(a.ws + L.bi) + r;
+    const double *g = a.gait + r * QLOCO_GAIT_MSG_LEN;
+    // callbacks (:79-110)
+    const int flag = (int)g[99];
+    double nrt[9];
+    for (int k = 0; k < 9; ++k) nrt[k] = g[86 + k];
+    if (ctrl[0] > 0) {
+      const int loop = R.I(I_LOOP) + 1;
+      R.I(I_LOOP) = loop;
+      const int t_int = (int)((uint32_t)R.I(I_TINT) + (uint32_t)(int)floor((double)(loop / 2)));
+      R.I(I_TINT) = t_int;
+      R.D(F_NRT + 0) = t_int;  // state_to_MPC = state_feedback (:519-527)
+      for (int k = 1; k < 25; ++k) R.D(F_NRT + k) = ctrl[k];
+      if (flag > 0) {
+        const int mpc = R.I(I_MPC) + 1;
+        R.I(I_MPC) = mpc;
+        int t_end = R.I(I_TEND);
+        interpolation(a, R, g, flag, t_int, t_end);
+        if (mpc * DT_FAST > 1.0) {  // _height_offset_timex = 1 (:537-545)
+          const int foot_i = (int)(mpc - (int)1.0 / DT_FAST);
+          int bjx1 = (int)body[26], bjxx = R.I(I_BJXX);
+          int sxx[NH], sx1[NH];
+          foot_traj_mod2(R, foot_i, nrt, bjx1, bjxx, t_end, sxx, sx1);
+          foot_rotation(R, foot_i, bjx1, bjxx, t_end, sxx, sx1);
+          body[26] = bjx1;
+          R.I(I_BJXX) = bjxx;
+          R.I(I_TEND) = t_end;
+        }
+        R.D(F_ZMP + 8) = 0.0;  // zmpxyz_ref(2) = _Zsc = {l,r}foot_inter(2) = 0 (:557-566)
+        // body_thetax(0..1) = bodyangle_mpc_ref(:, 0) (:590-591)
+        R.D(F_BTHX + 0) = (R.D(F_FTHETA + 0) + R.D(F_FTHETA + 3)) / 5;
+        R.D(F_BTHX + 1) = (R.D(F_FTHETA + 1) + R.D(F_FTHETA + 4)) / 5;
+        *bi = mpc;
+        do_body = 1;
+      }
+    }
+    *(reinterpret_cast<int32_t *>(a.ws + L.run) + r) = do_body;
+  }
+  // the reference record of every robot (read by body_mpc_kernel only where
+  // run = 1), written row-coalesced
+  stage_rows<PRE_T>(stage, tid, nb, r0, live, RF_USED, reinterpret_cast<double *>(a.ws + L.ref),
+                    RF_LD, 0, [&](int k) { return ref_slot(R, ctrl, k); });
+}
+
+// /rtMPC/traj slot k in [36, 100) of robot R: low_mpc_gait_inte(k - 36)
+// (gait_fast.cpp:633-714), the untouched [87, 98), (int)_tx_total/0.001 and
+// the loop count (:727-729)
+__device__ __forceinline__ double traj_slot(const Robot &R, const double *body,
+                                            const double *g, int k) {
+  const int u = k - 36;
+  if (u < 3) return R.D(F_RPY + u);                       // rpy_mpc_body
+  if (u < 5) return R.D(F_BTHX + u - 3);                  // body_thetax(0..1)
+  if (u == 5) return 0.0;                                 // body_thetax(2)
+  if (u < 9) return R.D(F_FOORPR + 3 + (u - 6));          // left foot
+  if (u < 12) return R.D(F_FOORPR + (u - 9));             // right foot
+  if (u < 14) return R.D(F_ZINT + u - 12);                // zmp_inter(0..1)
+  if (u == 14) return R.D(F_ZMP + 8);                     // zmpxyz_ref(2)
+  if (u < 27) return 0.0;                                 // F_L, F_R, M_L, M_R
+  if (u == 27) return g[27];                              // bjx1 of /MPC/Gait
+  if (u < 31) return R.D(F_FTHETA + 3 + (u - 28));        // left foot rpy
+  if (u < 34) return R.D(F_FTHETA + (u - 31));            // right foot rpy
+  if (u < 36) return R.D(F_DINT + u - 34);                // dcm_inter(0..1)
+  if (u < 50) return body[12 + (u - 36)];                 // bodyangle_mpc
+  if (u == 50) return 0.0;                                // t_fast_mpc (wall clock)
+  if (k < 98) return 0.0;
+  if (k == 98) return (int)R.D(F_TXTOT) / 0.001;          // (int) _tx_total / t_program_cyclic
+  return R.I(I_LOOP);                                     // count_in_rt_loop
+}
+
+constexpr int POST_T = 256;  // robots per block
+
+// Each lane computes its robot's slots; the block then writes the rows of its
+// robots cooperatively (a per-lane row store touches 64 lines per
+// instruction, the staged store 2-3).
+__global__ __launch_bounds__(POST_T) void rt_post_kernel(const RtArgs a) {
+  __shared__ double stage[POST_T * STG_LD];
+  const int tid = threadIdx.x;
+  const int64_t B = a.B, r0 = (int64_t)blockIdx.x * POST_T;
+  const int nb = (int)((B - r0) < POST_T ? (B - r0) : POST_T);
+  const int64_t r = r0 + tid;
+  const bool live = tid < nb;
   const Ws L = layout(B);
   Robot R{reinterpret_cast<double *>(a.ws + L.d) + r, reinterpret_cast<int32_t *>(a.ws + L.n) + r, B};
   const double *body = reinterpret_cast<const double *>(a.ws + L.body) + r * QLOCO_BODY_STATE_LEN;
-  const int32_t run = *(reinterpret_cast<const int32_t *>(a.ws + L.run) + r);
-  const int32_t bst = *(reinterpret_cast<const int32_t *>(a.ws + L.st) + r);
   const double *g = a.gait + r * QLOCO_GAIT_MSG_LEN;
-  const double *ctrl = a.ctrl + r * QLOCO_CTRL_MSG_LEN;
-  double *t = a.traj + r * QLOCO_TRAJ_MSG_LEN;
-  // /rtMPC/traj: [0,36) = /MPC/Gait[0,36), [36,87) = low_mpc_gait_inte (:633-724)
-  for (int k = 0; k < 36; ++k) t[k] = g[k];
-  double *u = t + 36;
-  for (int k = 0; k < 3; ++k) u[k] = R.D(F_RPY + k);
-  u[3] = R.D(F_BTHX + 0);
-  u[4] = R.D(F_BTHX + 1);
-  u[5] = 0.0;
-  u[6] = R.D(F_FOORPR + 3);
-  u[7] = R.D(F_FOORPR + 4);
-  u[8] = R.D(F_FOORPR + 5);
-  u[9] = R.D(F_FOORPR + 0);
-  u[10] = R.D(F_FOORPR + 1);
-  u[11] = R.D(F_FOORPR + 2);
-  u[12] = R.D(F_ZINT + 0);
-  u[13] = R.D(F_ZINT + 1);
-  u[14] = R.D(F_ZMP + 8);
-  for (int k = 15; k < 27; ++k) u[k] = 0.0;  // F_L, F_R, M_L, M_R
-  u[27] = g[27];
-  u[28] = R.D(F_FTHETA + 3);
-  u[29] = R.D(F_FTHETA + 4);
-  u[30] = R.D(F_FTHETA + 5);
-  u[31] = R.D(F_FTHETA + 0);
-  u[32] = R.D(F_FTHETA + 1);
-  u[33] = R.D(F_FTHETA + 2);
-  u[34] = R.D(F_DINT + 0);
-  u[35] = R.D(F_DINT + 1);
-  // bodyangle_mpc = body_theta_mpc's return = the record's last com_traj
-  for (int k = 0; k < 14; ++k) u[36 + k] = body[12 + k];
-  u[50] = 0.0;                                           // t_fast_mpc (wall clock)
-  for (int k = 87; k < 98; ++k) t[k] = 0.0;
-  t[98] = (int)R.D(F_TXTOT) / 0.001;  // (int) _tx_total / gait::t_program_cyclic
-  t[99] = R.I(I_LOOP);
-  double *n = a.nrt + r * QLOCO_NRT_MSG_LEN;
-  for (int k = 0; k < 25; ++k) n[k] = R.D(F_NRT + k);
-  if (a.gen) {
-    double *o = a.gen + r * 60;
-    for (int k = 0; k < 30; ++k) o[k] = R.D(F_FOORPR + k);
-    for (int k = 0; k < 30; ++k) o[30 + k] = R.D(F_FTHETA + k);
+  // [0, 36): the /MPC/Gait rows copied through (:716-719)
+  for (int idx = tid; idx < nb * 36; idx += POST_T) {
+    const int rr = idx / 36, k = idx - rr * 36;
+    a.traj[(r0 + rr) * QLOCO_TRAJ_MSG_LEN + k] = a.gait[(r0 + rr) * QLOCO_GAIT_MSG_LEN + k];
   }
-  if (a.sched) {
-    int32_t *s = a.sched + r * QLOCO_RT_SCHED_LEN;
-    s[0] = (int32_t)body[26];
-    s[1] = R.I(I_BJXX);
-    s[2] = R.I(I_TEND);
-    s[3] = R.I(I_MPC);
-    s[4] = R.I(I_TINT);
-    s[5] = run ? bst : -1;
-    s[6] = ctrl[0] > 0 ? 1 : 0;
-    s[7] = (int32_t)body[27];
+  stage_rows<POST_T>(stage, tid, nb, r0, live, 64, a.traj, QLOCO_TRAJ_MSG_LEN, 36,
+            [&](int k) { return traj_slot(R, body, g, 36 + k); });
+  // /rt2nrt/state (last published state_to_MPC)
+  stage_rows<POST_T>(stage, tid, nb, r0, live, 25, a.nrt, QLOCO_NRT_MSG_LEN, 0,
+            [&](int k) { return R.D(F_NRT + k); });
+  if (a.gen)  // debug dump: foorpr_gen | foortheta_gen (contiguous fields)
+    stage_rows<POST_T>(stage, tid, nb, r0, live, 60, a.gen, 60, 0,
+              [&](int k) { return R.D(F_FOORPR + k); });
+  if (a.sched && live) {
+    const int32_t run = *(reinterpret_cast<const int32_t *>(a.ws + L.run) + r);
+    const int32_t bst = *(reinterpret_cast<const int32_t *>(a.ws + L.st) + r);
+    const double *ctrl = a.ctrl + r * QLOCO_CTRL_MSG_LEN;
+    int32_t *sp = a.sched + r * QLOCO_RT_SCHED_LEN;
+    sp[0] = (int32_t)body[26];
+    sp[1] = R.I(I_BJXX);
+    sp[2] = R.I(I_TEND);
+    sp[3] = R.I(I_MPC);
+    sp[4] = R.I(I_TINT);
+    sp[5] = run ? bst : -1;
+    sp[6] = ctrl[0] > 0 ? 1 : 0;
+    sp[7] = (int32_t)body[27];
   }
 }
 
@@ -685,20 +763,22 @@ extern "C" int qloco_rt_tick(int64_t batch, void *workspace, const double *gait_
   a.sched = sched;
   rt::aaa_inv_mod(a.aaa_inv_mod);
   const hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)((batch + 255) / 256));
-  hipLaunchKernelGGL(rt::rt_pre_kernel, grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL(rt::rt_pre_kernel, dim3((unsigned)((batch + rt::PRE_T - 1) / rt::PRE_T)),
+                     dim3(rt::PRE_T), 0, s, a);
   QLOCO_HIP_CHECK(hipGetLastError(), "rt_pre_kernel launch");
   const rt::Ws L = rt::layout(batch);
   char *w = (char *)workspace;
   const int rc = body_mpc_launch(
-      batch, (const int32_t *)(w + L.bi), (const double *)(w + L.bas),
-      (const double *)(w + L.zmp), (const double *)(w + L.ang), (const double *)(w + L.rft),
-      (const double *)(w + L.lft), (const double *)(w + L.acc), (double *)(w + L.body),
+      batch, (const int32_t *)(w + L.bi), (const double *)(w + L.ref) + rt::RF_BAS,
+      (const double *)(w + L.ref) + rt::RF_ZMP, (const double *)(w + L.ref) + rt::RF_ANG,
+      (const double *)(w + L.ref) + rt::RF_RFT, (const double *)(w + L.ref) + rt::RF_LFT,
+      (const double *)(w + L.ref) + rt::RF_ACC, (double *)(w + L.body),
       (double *)(w + L.ct), (int32_t *)(w + L.st),
       (const double *)(w + L.d) + (int64_t)rt::F_TX * batch, batch,
-      (const int32_t *)(w + L.run), s);
+      (const int32_t *)(w + L.run), rt::RF_LD, s);
   if (rc != QLOCO_OK) return rc;
-  hipLaunchKernelGGL(rt::rt_post_kernel, grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL(rt::rt_post_kernel, dim3((unsigned)((batch + rt::POST_T - 1) / rt::POST_T)),
+                     dim3(rt::POST_T), 0, s, a);
   QLOCO_HIP_CHECK(hipGetLastError(), "rt_post_kernel launch");
   return QLOCO_OK;
 }

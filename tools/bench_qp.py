@@ -1,0 +1,122 @@
+"""Measurement for SURVEY.md §8f row 1 / §8a rows a8-a11 (batched Go1 force
+distribution QP, Dynamiccclass::force_distribution + force_opt, servo.cpp:
+1224-1228): one JSON line with QP solves/s, the fp64 compute roofline and the
+C restatement timed beside it.
+
+    python tools/bench_qp.py [--robots B] [--steps K] [--warmup W]
+
+Workload: B robots (default 65536), one qloco_force_qp_solve launch per step
+(force_distribution heuristic + G/g0/CE/CI build + quirk-compatible
+Goldfarb-Idnani, n = 12, p = 12 (6 live or 0), m = 24, fp64), inputs
+resident in HBM (tests/cases.force_inputs: mixed modes 101/102/103 and
+right_support 0/1/2), member state (grf_opt = F_prev, F_leg_ref) carried
+between steps exactly as the servo's Dynamiccclass.
+Algorithmic fp64 flops per solve (EiQuadProg.cpp structure, K = measured
+active-set iterations): build A'A 2*6*12*12 = 1728, LLT n^3/3 = 576,
+J = L^-T n^3/3 = 576, x0 2n^2 = 288, per iteration 2nm + 10n^2 = 2016.
+Peak: 78.6 TFLOP/s fp64 vector (MI355X spec sheet; MICROARCH.md lists no
+fp64 figure).  The kernel is latency-bound (one QP per 16-lane group, short
+dependent chains), so the fraction is small by construction.
+cpu_baseline: oracle/force_qp.c qo_force_batch, 1 thread, bounded sample.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+PEAK_FP64_TFLOPS = 78.6
+N, M = 12, 24
+
+
+def flops(iters):
+    return 1728 + N ** 3 / 3 + N ** 3 / 3 + 2 * N * N + iters * (2 * N * M + 10 * N * N)
+
+
+def cpu_baseline(inp, budget_s=6.0):
+    import oracle_lib as O
+    L = O.lib()
+    L.qo_force_batch.argtypes = [C.c_int64, C.c_void_p, C.POINTER(O.ForceParams)] + [C.c_void_p] * 12
+    prm = O.ForceParams()
+    L.qo_force_params_default(C.byref(prm))
+    n = 4096
+    states = (O.DynState * n)()
+    for s in states:
+        L.qo_dyn_init(C.byref(s))
+    arr = {k: np.ascontiguousarray(v[:n]) for k, v in inp.items()}
+    out = np.zeros((n, 12))
+    solves, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        L.qo_force_batch(n, C.cast(states, C.c_void_p), C.byref(prm),
+                         *[arr[k].ctypes.data for k in ("com_des", "leg_des", "F_force_des",
+                                                        "rfoot_des", "lfoot_des", "base_p",
+                                                        "feet_p", "FT_total_des", "mode",
+                                                        "right_support", "y_coef")],
+                         out.ctypes.data)
+        solves += n
+    dt = time.perf_counter() - t0
+    for s in states:
+        L.qo_dyn_free(C.byref(s))
+    return solves / dt, "%d robots x %d calls" % (n, solves // n)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--robots", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    import torch
+    from cases import force_inputs
+    from quadrupedal_loco_amd import qp
+    B = args.robots
+    dev = torch.device("cuda:0")
+    inp = force_inputs(np.random.default_rng(3), B)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in inp.items()}
+    solver = qp.ForceQP(batch=B, device=dev)
+    for _ in range(args.warmup):
+        out = solver.step(**d)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    ev[0].record(stream)
+    for k in range(args.steps):
+        out = solver.step(**d)
+        ev[k + 1].record(stream)
+    torch.cuda.synchronize()
+    per = np.array([ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)])
+    ms = float(per.mean())
+    iters = out["iters"].cpu().numpy()
+    status = out["status"].cpu().numpy()
+    f = float(flops(iters.astype(np.float64)).sum())
+    achieved = f / (ms * 1e-3) / 1e12
+    line = {"metric": "Go1 force-distribution QP solves/sec (Dynamiccclass force_distribution + "
+                      "force_opt, EiQuadProg fp64)",
+            "value": B / (ms * 1e-3), "unit": "solves/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms,
+            "p99_batch_us": float(np.percentile(per, 99) * 1e3), "higher_is_better": True,
+            "dtype": "f64", "data": "synthetic (tests/cases.force_inputs, seed 3)",
+            "config": {"workload": "force QP, %d robots, modes 101/102/103, right_support 0/1/2" % B},
+            "gi_iters_mean": float(iters.mean()), "status_ok_frac": float(np.mean(status == 0)),
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS,
+                         "traffic": None,
+                         "note": "fp64 VALU (no MFMA on this path); algorithmic flops per solve "
+                                 "in the tool docstring; latency-bound active set"}}
+    if not args.no_cpu_baseline:
+        v, sample = cpu_baseline(inp)
+        line["cpu_baseline"] = {"value": v, "unit": "solves/s", "cores": 1, "kind": "port",
+                                "sample": sample + ", oracle/force_qp.c qo_force_batch"}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
