@@ -149,7 +149,7 @@ __constant__ BodyConsts c_body_K;
 
 struct BodyLds {
   struct Grp {
-    double G[BNT * BNT], g0[BNT], ci0[BNI], x[16];
+    double g0[BNT], ci0[BNI], x[BNT];  // G is built in gi.R (see qloco_gi_core.hpp)
     GiLdsT<BNT, BNI, 0> gi;
   } g[GI_GROUPS];
 };
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
     double pth[BNH];
     for (int jx = 0; jx < BNH; jx++) pth[jx] = K.j_ini / (K.mass * (R3(comacc_ref, 2, jx) + K.g));
     if (li == 0) {
-      for (int t = 0; t < BNT * BNT; ++t) P.G[t] = 0.0;
+      for (int t = 0; t < BNT * BNT; ++t) P.gi.R[t] = 0.0;
       for (int c = 0; c < BNH; ++c)
         for (int r = 0; r < BNH; ++r) {  // :511-515
           const double I = (r == c) ? 1.0 : 0.0;
@@ -235,8 +235,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
                             K.beltathetax / 2 * K.ppu_2[c * BNH + r] + K.gama_zmpy / 2 * pp;
           const double wy = K.Rthetay / 2 * I + K.alphathetay / 2 * K.pvu_2[c * BNH + r] +
                             K.beltathetay / 2 * K.ppu_2[c * BNH + r] + K.gama_zmpx / 2 * pp;
-          P.G[c * BNT + r] = 2 * wx;
-          P.G[(c + BNH) * BNT + (r + BNH)] = 2 * wy;
+          P.gi.R[c * BNT + r] = 2 * wx;
+          P.gi.R[(c + BNH) * BNT + (r + BNH)] = 2 * wy;
         }
       double det_px[BNH], det_py[BNH];
       for (int k = 0; k < BNH; ++k) {
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
     GI_SYNC();
     double f;
     int it;
-    gi_solve_group(P.gi, li, BNT, 0, BNI, P.G, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
+    gi_solve_group(P.gi, li, BNT, 0, BNI, P.gi.R, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
                    status, it);
     GI_SYNC();
     if (li == 0) {

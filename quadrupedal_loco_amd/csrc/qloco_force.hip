@@ -11,6 +11,8 @@
 // (:305) are reproduced; a NaN solution falls back to F_leg_guess (:364-367).
 #include <string.h>
 
+#include <mutex>
+
 #include "qloco_gi_core.hpp"
 
 namespace qloco {
@@ -25,12 +27,22 @@ struct ForceArgs {
   int *qp_solution, *status, *iters;
 };
 
+// The swing-leg equality patterns AA (dynmics_compute.cpp:310-350): 0 = none
+// (rs = 2 or other modes), 1 = mode 102 rs 0 (FL, RR zero), 2 = mode 102
+// rs 1 (FR, RL), 3 = mode 101 rs 0 (FR, RR), 4 = mode 101 rs 1 (FL, RL);
+// 12x12 column-major, in constant memory (identical for every robot).
+__constant__ double c_force_CE[5][144];
+
+// Per group: A (6x12) is built in the solver's J and G in its R (both are
+// free until the solve starts, and the solver reads only G's lower triangle,
+// copying it in place), so a 4-robot block needs ~18 KB of LDS: 8 blocks per
+// CU, 2 waves per SIMD.
 struct ForceLds {
   double CI[12 * 24];  // shared by the four groups (constant rows)
   double ci0[24];
   double zeros[16];
   struct Grp {
-    double G[144], g0[12], CE[144], A[72], x[16], guess[12];
+    double g0[12], x[16], guess[12];
     GiLdsT<12, 24, 12> gi;
   } g[GI_GROUPS];
 };
@@ -104,7 +116,8 @@ __device__ void force_distribution(const double *com_des, const double *leg_des,
 #undef FRC
 }
 
-__global__ __launch_bounds__(64) void force_qp_kernel(const ForceArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void force_qp_kernel(
+    const ForceArgs a) {
   __shared__ ForceLds S;
   const int lane = threadIdx.x, grp = lane >> 4, li = lane & 15;
   const int64_t inst = (int64_t)blockIdx.x * GI_GROUPS + grp;
@@ -135,6 +148,8 @@ __global__ __launch_bounds__(64) void force_qp_kernel(const ForceArgs a) {
   __syncthreads();
   if (inst >= a.batch) return;
   ForceLds::Grp &P = S.g[grp];
+  double *const PA = P.gi.J;  // A, 6x12 col-major (dead before J is formed)
+  double *const PG = P.gi.R;  // G, 12x12 col-major (the solver's LLT workspace)
 
   // ---- force_distribution (state F_leg_ref in/out) -> F_leg_guess
   double Fref[12];
@@ -145,7 +160,7 @@ __global__ __launch_bounds__(64) void force_qp_kernel(const ForceArgs a) {
   if (li < 12) P.guess[li] = Fref[li];
   // ---- force_opt: A (6x12, col-major) with the skew_hat quirk (:274-298)
   if (li < 12) {
-    for (int k = 0; k < 6; ++k) P.A[li * 6 + k] = 0.0;
+    for (int k = 0; k < 6; ++k) PA[li * 6 + k] = 0.0;
   }
   GI_SYNC();
   if (li < 4) {
@@ -153,61 +168,45 @@ __global__ __launch_bounds__(64) void force_qp_kernel(const ForceArgs a) {
     const double *bp = a.base_p + inst * 3;
     const double *fp = a.feet_p + inst * 12 + 3 * leg;
     const double v0 = bp[0] - fp[0];  // skew_hat uses vec_w[0] everywhere (comma operator)
-    for (int k = 0; k < 3; ++k) P.A[(3 * leg + k) * 6 + k] = 1.0;
+    for (int k = 0; k < 3; ++k) PA[(3 * leg + k) * 6 + k] = 1.0;
     // W rows [0,-a,a],[a,0,-a],[-a,a,0]
     const double W[3][3] = {{0.0, -v0, v0}, {v0, 0.0, -v0}, {-v0, v0, 0.0}};
     for (int r = 0; r < 3; ++r)
-      for (int k = 0; k < 3; ++k) P.A[(3 * leg + k) * 6 + 3 + r] = W[r][k];
+      for (int k = 0; k < 3; ++k) PA[(3 * leg + k) * 6 + 3 + r] = W[r][k];
   }
   GI_SYNC();
-  // G = 2 (alpha A'A + (beta+gamma) I), then (G' + G)/2 ; g0 (:300-305)
-  double Grow[12];
+  // G = 2 (alpha A'A + (beta+gamma) I), then (G' + G)/2 ; g0 (:300-305).
+  // A'A(r,c) and A'A(c,r) are the same products summed in the same order, so G
+  // is exactly symmetric and (G' + G)/2 = (x + x)/2 = x bit for bit: the
+  // symmetrisation is the identity and is not executed.
   if (li < 12) {
     const int r = li;
     for (int c = 0; c < 12; ++c) {
       double ata = 0.0;
-      for (int k = 0; k < 6; ++k) ata += P.A[r * 6 + k] * P.A[c * 6 + k];
-      Grow[c] = 2.0 * (a.alpha * ata + (r == c ? (a.beta + a.gamma) : 0.0));
+      for (int k = 0; k < 6; ++k) ata += PA[r * 6 + k] * PA[c * 6 + k];
+      PG[c * 12 + r] = 2.0 * (a.alpha * ata + (r == c ? (a.beta + a.gamma) : 0.0));
     }
-    for (int c = 0; c < 12; ++c) P.G[c * 12 + r] = Grow[c];  // column-major, entry (r,c)
   }
   GI_SYNC();
   if (li < 12) {
     const int r = li;
-    for (int c = 0; c < 12; ++c) Grow[c] = (P.G[r * 12 + c] + P.G[c * 12 + r]) / 2.0;
-  }
-  GI_SYNC();
-  if (li < 12) {
-    const int r = li;
-    for (int c = 0; c < 12; ++c) P.G[c * 12 + r] = Grow[c];
     double atf = 0.0;
     const double *FT = a.FT_total_des + inst * 6;
-    for (int k = 0; k < 6; ++k) atf += P.A[r * 6 + k] * FT[k];
+    for (int k = 0; k < 6; ++k) atf += PA[r * 6 + k] * FT[k];
     P.g0[r] = -2.0 * (a.alpha * atf + a.beta * P.guess[r] + a.gamma * a.grf_opt[inst * 12 + r]);
-    for (int c = 0; c < 12; ++c) P.CE[c * 12 + r] = 0.0;
   }
   GI_SYNC();
   // swing-leg equality pattern AA (:310-350)
-  if (li == 0) {
+  int pat = 0;
+  {
     const int mode = a.mode[inst], rs = a.right_support[inst];
-    int z0 = -1, z1 = -1;
-    if (mode == 102) {
-      if (rs == 0) { z0 = 1; z1 = 2; }
-      else if (rs == 1) { z0 = 0; z1 = 3; }
-    } else if (mode == 101) {
-      if (rs == 0) { z0 = 0; z1 = 2; }
-      else if (rs == 1) { z0 = 1; z1 = 3; }
-    }
-    if (z0 >= 0)
-      for (int k = 0; k < 3; ++k) {
-        P.CE[(3 * z0 + k) * 12 + 3 * z0 + k] = 1.0;
-        P.CE[(3 * z1 + k) * 12 + 3 * z1 + k] = 1.0;
-      }
+    if (mode == 102) pat = rs == 0 ? 1 : rs == 1 ? 2 : 0;
+    else if (mode == 101) pat = rs == 0 ? 3 : rs == 1 ? 4 : 0;
   }
-  GI_SYNC();
   double f;
   int st, it;
-  gi_solve_group(P.gi, li, 12, 12, 24, P.G, 12, P.g0, P.CE, S.zeros, S.CI, S.ci0, P.x, f, st, it);
+  gi_solve_group(P.gi, li, 12, 12, 24, PG, 12, P.g0, c_force_CE[pat], S.zeros, S.CI, S.ci0, P.x,
+                 f, st, it);
   GI_SYNC();
   // QPBaseClass::solveQP: success iff no NaN (:200-227); Solve / fallback
   bool ok = true;
@@ -215,7 +214,7 @@ __global__ __launch_bounds__(64) void force_qp_kernel(const ForceArgs a) {
   if (li < 12) {
     a.grf_opt[inst * 12 + li] = ok ? P.x[li] : P.guess[li];
     a.F_leg_guess[inst * 12 + li] = P.guess[li];
-    a.F_leg_ref[inst * 12 + li] = Fref[li];
+    a.F_leg_ref[inst * 12 + li] = P.guess[li];  // = Fref (F_leg_guess := F_leg_ref, :251-260)
   }
   if (li == 0) {
     if (a.qp_solution) a.qp_solution[inst] = ok ? 1 : 0;
@@ -264,6 +263,28 @@ extern "C" void qloco_force_params_default(qloco_force_params *p) {
   p->mu = 0.25;
 }
 
+// c_force_CE, once per device
+static int force_ce_upload() {
+  static std::mutex mu;
+  static bool done[256] = {};
+  int dev = 0;
+  QLOCO_HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
+  std::lock_guard<std::mutex> lock(mu);
+  if (dev >= 0 && dev < 256 && done[dev]) return QLOCO_OK;
+  double CE[5][144];
+  memset(CE, 0, sizeof(CE));
+  const int zz[5][2] = {{-1, -1}, {1, 2}, {0, 3}, {0, 2}, {1, 3}};
+  for (int q = 1; q < 5; ++q)
+    for (int k = 0; k < 3; ++k) {
+      const int z0 = zz[q][0], z1 = zz[q][1];
+      CE[q][(3 * z0 + k) * 12 + 3 * z0 + k] = 1.0;
+      CE[q][(3 * z1 + k) * 12 + 3 * z1 + k] = 1.0;
+    }
+  QLOCO_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_force_CE), CE, sizeof(CE)), "c_force_CE upload");
+  if (dev >= 0 && dev < 256) done[dev] = true;
+  return QLOCO_OK;
+}
+
 extern "C" int qloco_force_qp_solve(const qloco_force_params *prm, int64_t batch,
                                     const double *com_des, const double *leg_des,
                                     const double *F_force_des, const double *rfoot_des,
@@ -305,6 +326,8 @@ extern "C" int qloco_force_qp_solve(const qloco_force_params *prm, int64_t batch
   a.qp_solution = qp_solution;
   a.status = status;
   a.iters = iters;
+  const int rc = force_ce_upload();
+  if (rc != QLOCO_OK) return rc;
   const unsigned blocks = (unsigned)((batch + GI_GROUPS - 1) / GI_GROUPS);
   hipLaunchKernelGGL(force_qp_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
   QLOCO_HIP_CHECK(hipGetLastError(), "force_qp_kernel launch");

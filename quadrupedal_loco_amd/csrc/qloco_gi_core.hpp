@@ -19,15 +19,18 @@ constexpr int GI_GROUPS = 4;             // instances per wavefront
 // Per-group LDS work space, sized for at most NN variables, MM inequalities
 // and PP equalities (the generic kernel uses the GI_* limits; the force and
 // body kernels instantiate their exact sizes so more groups fit per CU).
+// The active set never holds more than max(n, p) + 1 entries (equality i is
+// recorded at index i < p, the quirk of EiQuadProg.cpp:268; inequalities at
+// iq <= n), so A/u/r are sized AS; iai/iaexcl are indexed by constraint.
 template <int NN, int MM, int PP>
 struct GiLdsT {
-  static constexpr int PMM = PP + MM + 1;
+  static constexpr int AS = (NN > PP ? NN : PP) + 1;
   double J[NN * NN];  // col-major, J(r,c) = J[c*NN + r]
   double R[NN * NN];
   double x[NN], z[NN], d[NN], np[NN], xold[NN];
   double s[MM];
-  double r[PMM], u[PMM], uold[PMM];
-  int A[PMM], Aold[PMM], iai[PMM], iaexcl[PMM];
+  double r[AS], u[AS], uold[AS];
+  int A[AS], Aold[AS], iai[MM], iaexcl[MM];
 };
 using GiLds = GiLdsT<GI_N, GI_M, GI_P>;
 
@@ -241,20 +244,25 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
   int iter = 0;
   double f_value = 0.0;
   // persistent-member semantics: start every solve from zeroed index arrays
-  for (int k = li; k < (PP + MM + 1); k += 16) {
+  for (int k = li; k < GiLdsT<NN, MM, PP>::AS; k += 16) {
     S.A[k] = 0;
     S.Aold[k] = 0;
-    S.iai[k] = 0;
-    S.iaexcl[k] = 0;
     S.u[k] = 0.0;
     S.r[k] = 0.0;
     S.uold[k] = 0.0;
   }
+  for (int k = li; k < MM; k += 16) {
+    S.iai[k] = 0;
+    S.iaexcl[k] = 0;
+  }
   // ---- solve_quadprog: c1 = trace(G); LLT of the lower triangle (EiQuadProg.cpp:493-513)
   double c1 = 0.0;
   for (int i = 0; i < n; ++i) c1 += G[i * ldG + i];
-  // L is built in R (zeroed again before solve_quadprog2 uses R)
-  for (int k = li; k < NN * NN; k += 16) S.R[k] = 0.0;
+  // L is built in R (zeroed again before solve_quadprog2 uses R).  Only the
+  // lower triangle is read before that, so a caller may build G in S.R itself
+  // (ldG = NN): the copy below is then in place and the clear is skipped.
+  if (G != S.R)
+    for (int k = li; k < NN * NN; k += 16) S.R[k] = 0.0;
   GI_SYNC();
   if (li < n)
     for (int c = 0; c <= li; ++c) S.R[c * NN + li] = G[c * ldG + li];  // lower triangle, row li
