@@ -217,8 +217,12 @@ __device__ void recompute_tx(const Robot &R) {  // :1773-1779
 // through (in1, in2, ref, ref2) at t = -dt, 0, dt, 2dt (dt = dt_mpc_slow)
 __device__ void position_mod3(const RtArgs &a, const Robot &R, int walktime, int f_in,
                               int f_out, int t_end) {
-  for (int k = 0; k < 21; ++k) R.D(f_out + k) = 0.0;
-  if (walktime > t_end) return;
+  // com_inte.setZero(): entries 18..20 are never written below (jx < 4) and
+  // stay 0 from init; 0..17 are all overwritten
+  if (walktime > t_end) {
+    for (int k = 0; k < 21; ++k) R.D(f_out + k) = 0.0;
+    return;
+  }
   double in[4][3];
   for (int q = 0; q < 4; ++q)
     for (int ax = 0; ax < 3; ++ax) in[q][ax] = R.D(f_in + 3 * q + ax);
@@ -295,8 +299,13 @@ __device__ void foot_traj_mod2(const Robot &R, int j_indexx, const double nrt[9]
     R.fxyz(2, bjxx_nrt + 1) = nrt[6];
   }
   const int bjx_period_nrt = (int)nrt[7];
-  if (nrt[8] > 0 && bjx_period_nrt >= 0 && bjx_period_nrt < NS) R.D(F_TS + bjx_period_nrt) = nrt[8];
-  recompute_tx(R);
+  // _td and _tx are pure functions of _ts (:1773-1779), recomputed by the
+  // reference on every call; they only change when this call changed _ts
+  if (nrt[8] > 0 && bjx_period_nrt >= 0 && bjx_period_nrt < NS &&
+      R.D(F_TS + bjx_period_nrt) != nrt[8]) {
+    R.D(F_TS + bjx_period_nrt) = nrt[8];
+    recompute_tx(R);
+  }
   t_end = (int)round((R.D(F_TX + NS - 1) - 2 * TSTEP) / DT_FAST);  // :1780
   R.D(F_TXTOT) = R.D(F_TX + NS - 1);
   IndexScan scan;  // goals j*dt, (j+1)*dt, (j+1)*dt, ... never decrease
