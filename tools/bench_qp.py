@@ -40,6 +40,14 @@ def flops(iters):
     return 1728 + N ** 3 / 3 + N ** 3 / 3 + 2 * N * N + iters * (2 * N * M + 10 * N * N)
 
 
+def _traffic(B):
+    f = os.path.join(ROOT, "profiles", "traffic_force_qp_b%d.json" % B)
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        return json.load(fh).get("hbm_bytes_per_launch_raw")
+
+
 def cpu_baseline(inp, budget_s=6.0):
     import oracle_lib as O
     L = O.lib()
@@ -108,7 +116,7 @@ def main():
             "gi_iters_mean": float(iters.mean()), "status_ok_frac": float(np.mean(status == 0)),
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS,
-                         "traffic": None,
+                         "traffic": _traffic(B),
                          "note": "fp64 VALU (no MFMA on this path); algorithmic flops per solve "
                                  "in the tool docstring; latency-bound active set"}}
     if not args.no_cpu_baseline:

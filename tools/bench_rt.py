@@ -12,9 +12,16 @@ body_theta_mpc, /rtMPC/traj + /rt2nrt/state).  M message sets
 HBM before the timed region; step t uses set t mod M.  W warm-up ticks
 (default 150) run first so every robot is past the 1 s height-offset phase
 and into foot generation + body MPC (count_in_rt_mpc > 100).
-Algorithmic HBM bytes per robot-tick (fp64): messages in 125 x 8 = 1000,
-messages out 125 x 8 = 1000, node state read + written 2 x (551 x 8 + 7 x 4
-+ 32 x 8) = 9384 -> 11384 B.  Peak 8.0 TB/s (MI355X_MICROARCH.md).
+Algorithmic HBM bytes per robot-tick (fp64), with foot generation running
+(the steady state): messages in 125 x 8 = 1000 and out 125 x 8 = 1000; the
+live node state the reference's loop reads (interpolation knots 48, swing
+foot arrays 108, footholds 12, _tx scan 27, _ts/_td 8, lift 4, foot
+rotation 8, body-MPC record 32, misc 2 = 249 doubles + 7 ints) and writes
+(interpolation outputs 72 + knot shifts 24 (every other tick), foot arrays
+108, footholds 6, foot rotation 8, generator outputs 60, /rt2nrt 25, body
+record 32 = 335 doubles + 7 ints) = 4728 B -> 6728 B per robot-tick.
+Peak 8.0 TB/s (MI355X_MICROARCH.md).  `traffic` = measured HBM bytes per
+tick (profiles/traffic_rt_tick_b65536.json, FETCH_SIZE / WRITE_SIZE passes).
 cpu_baseline: oracle/rt_tick.c (qo_rt_tick_n), 1 thread, bounded sample.
 """
 import argparse
@@ -30,8 +37,17 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0
-BYTES_PER_ROBOT_TICK = 1000 + 1000 + 2 * (551 * 8 + 7 * 4 + 32 * 8)
+BYTES_PER_ROBOT_TICK = 1000 + 1000 + (249 + 335) * 8 + 2 * 7 * 4
 SEED = 20261016
+
+
+def _traffic(B):
+    """measured HBM bytes per tick (raw FETCH_SIZE + WRITE_SIZE) if profiled at this B"""
+    f = os.path.join(ROOT, "profiles", "traffic_rt_tick_b%d.json" % B)
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        return json.load(fh).get("hbm_bytes_per_tick_raw")
 
 
 def cpu_baseline(sets, budget_s=8.0):
@@ -84,7 +100,7 @@ def main():
     wall = time.perf_counter() - t0
     per = np.array([ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)])
     ms = float(per.mean())
-    _, _, _, sched = node.tick(*sets[0])
+    _, _, _, sched = node.tick(*sets[(args.warmup + args.steps) % M])  # one more tick, for its counts
     sched = sched.cpu().numpy()
     achieved = BYTES_PER_ROBOT_TICK * B / (ms * 1e-3) / 1e9
     line = {"metric": "rt_mpc_qp node ticks/sec (gait_fast loop body + PRMPCClass generators "
@@ -101,7 +117,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_robot_tick": BYTES_PER_ROBOT_TICK,
-                         "traffic": None,
+                         "traffic": _traffic(B),
                          "note": "whole tick (3 launches) against the state-streaming bytes"}}
     if not args.no_cpu_baseline:
         v, sample = cpu_baseline(sets)
