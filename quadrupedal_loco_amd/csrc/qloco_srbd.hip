@@ -585,13 +585,19 @@ __device__ unsigned int g_phase[1 << 20];
 #ifndef QLOCO_SRBD_WAVES_PER_EU_W2  // two-wave kernel occupancy
 #define QLOCO_SRBD_WAVES_PER_EU_W2 2
 #endif
-#ifndef QLOCO_SRBD_WAVES_PER_EU  // one-wave kernel occupancy: 3 waves/SIMD = 168 VGPRs, ~no spills
-#define QLOCO_SRBD_WAVES_PER_EU 3
+#ifndef QLOCO_SRBD_WAVES_PER_EU  // one-wave kernel occupancy for large batches: 3 waves/SIMD
+#define QLOCO_SRBD_WAVES_PER_EU 3    // = 168 VGPRs (23 spills, all in setup / refactor paths)
 #endif
+// One-wave kernel, small batches (<= kSmallBatch instances, i.e. <= 6 waves
+// per SIMD over the launch): 2 waves/SIMD = 194 VGPRs, spill-free -- with few
+// waves per SIMD the tail of long instances dominates and more registers per
+// wave (no scratch round trips) beat the third resident wave.  Measured on
+// Go1 trot N = 10: B = 4096 307 vs 314 us, B = 8192 539 vs 505 us.
+constexpr int64_t kSmallBatch = 6144;
 
-template <int W>
+template <int W, int WPE>
 __global__ __launch_bounds__(64 * W)
-__attribute__((amdgpu_waves_per_eu(W == 1 ? QLOCO_SRBD_WAVES_PER_EU : QLOCO_SRBD_WAVES_PER_EU_W2)))
+__attribute__((amdgpu_waves_per_eu(WPE)))
 void srbd_admm_kernel(const SrbdArgs a) {
   constexpr int NC = 64 * W, NQ = 16 * W;
   __shared__ __attribute__((aligned(16))) SrbdLds<W> S;
@@ -1317,15 +1323,23 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   hipStream_t st = (hipStream_t)stream;
   a.leg_lo = 0;
   a.leg_hi = 1 << 30;
+  auto launch_w1 = [&]() {
+    if (batch <= kSmallBatch)
+      hipLaunchKernelGGL((srbd_admm_kernel<1, 2>), dim3((unsigned)batch), dim3(64), 0, st, a);
+    else
+      hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU>), dim3((unsigned)batch),
+                         dim3(64), 0, st, a);
+  };
   if (legs <= kLegsPerWave) {
-    hipLaunchKernelGGL(srbd_admm_kernel<1>, dim3((unsigned)batch), dim3(64), 0, st, a);
+    launch_w1();
   } else {
     a.leg_hi = kLegsPerWave;
-    hipLaunchKernelGGL(srbd_admm_kernel<1>, dim3((unsigned)batch), dim3(64), 0, st, a);
+    launch_w1();
     QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel<1> launch");
     a.leg_lo = kLegsPerWave + 1;
     a.leg_hi = 1 << 30;
-    hipLaunchKernelGGL(srbd_admm_kernel<2>, dim3((unsigned)batch), dim3(128), 0, st, a);
+    hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2>), dim3((unsigned)batch),
+                       dim3(128), 0, st, a);
   }
   QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel launch");
   return QLOCO_OK;
