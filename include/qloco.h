@@ -278,6 +278,36 @@ int qloco_rt_tick(int64_t batch, void *workspace, const double *gait_msg,
                   const double *ctrl_msg, double *traj_msg, double *nrt_msg, double *gen,
                   int32_t *sched, void *stream);
 
+/* ====================================================================== */
+/* 7. go1 servo force block, batched                */
+/*    replaces servo.cpp:1052-1243 (+ :1318) of go1_rt_control: leg        */
+/*    positions, body-relative desired feet and their velocity, F_sum,      */
+/*    rleg_com / F_lr_predict, swing flags, then Dynamiccclass::            */
+/*    force_distribution + force_opt and compute_joint_torques x 4          */
+/* ====================================================================== */
+/* Per-robot inputs (device, double unless noted), legs FR, FL, RR, RL:
+ *   coma_des[B*3], com_des[B*3], rfoot_des[B*3], lfoot_des[B*3],
+ *   body_p_des[B*3], foot_des[B*12] (desired feet, world frame),
+ *   right_support[B], gait_mode[B], loop_count[B] (int32; count_in_rt_loop),
+ *   y_offset[B], Jaco[B*4*9] (each leg's 3x3 Jacobian_kin, col-major),
+ *   foot_rel_mea[B*12] (measured foot - body), v_est_rel[B*12].
+ * Outputs: grf_opt[B*12] and tau[B*12] (Legs_torque) required; F_sum[B*6],
+ *   Force_L_R[B*6] (F_lr_predict), swing[B*4], qp_solution[B], status[B]
+ *   optional.  Member / loop state (F_leg_ref, grf_opt, swing flags,
+ *   relative_des_old, v_relative) lives in the workspace. */
+int64_t qloco_servo_workspace_bytes(int64_t batch);
+int qloco_servo_init(int64_t batch, void *workspace, void *stream);
+int qloco_servo_force_block(const qloco_force_params *prm, int64_t batch, void *workspace,
+                            const double *coma_des, const double *com_des,
+                            const double *rfoot_des, const double *lfoot_des,
+                            const double *body_p_des, const double *foot_des,
+                            const int32_t *right_support, const int32_t *gait_mode,
+                            const double *y_offset, const int32_t *loop_count,
+                            const double *Jaco, const double *foot_rel_mea,
+                            const double *v_est_rel, double *F_sum, double *Force_L_R,
+                            double *grf_opt, double *tau, int32_t *swing,
+                            int32_t *qp_solution, int32_t *status, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -164,6 +164,36 @@ void qo_rt_tick_n(qo_rt *arr, int64_t n, const double *gait, const double *ctrl,
 void qo_inv4(const double A[16], double Ainv[16]);
 
 /* ------------------------------------------------------------------ */
+/* go1 servo force block: servo.cpp:1052-1243, :1318 (servo_block.c)    */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  qo_dyn_state dyn;      /* Dynamiccclass members (F_leg_ref, grf_opt, QP object) */
+  int swing[4];          /* FR_swing, FL_swing, RR_swing, RL_swing */
+  double rel_des_old[12];/* *_foot_relative_des_old */
+  double v_rel[12];      /* *_v_relative */
+} qo_servo_state;
+void qo_servo_init(qo_servo_state *s);
+void qo_servo_free(qo_servo_state *s);
+/* One servo tick's force block for one robot; legs FR, FL, RR, RL; Jaco 4 x
+ * (3x3 col-major).  Outputs F_sum, Force_L_R (F_lr_predict), rleg_com
+ * (optional), grf_opt (force_opt result), tau (12), swing flags (optional).
+ * Returns qp_solution. */
+int qo_servo_force_block(qo_servo_state *s, const qo_force_params *prm, const double coma_des[3],
+                         const double com_des[3], const double rfoot_des[3],
+                         const double lfoot_des[3], const double body_p_des[3],
+                         const double foot_des[12], int right_support, int gait_mode,
+                         double y_offset, int loop_count, const double Jaco[36],
+                         const double rel_mea[12], const double v_est[12], double F_sum[6],
+                         double Force_L_R[6], double *rleg_com_out, double grf_opt[12],
+                         double tau[12], int swing_out[4], int *eqp_status);
+void qo_servo_batch(int64_t n, qo_servo_state *states, const qo_force_params *prm,
+                    const double *coma, const double *com, const double *rfoot,
+                    const double *lfoot, const double *body_p, const double *foot,
+                    const int32_t *rs, const int32_t *mode, const double *y,
+                    const int32_t *loop, const double *Jaco, const double *rel_mea,
+                    const double *v_est, double *grf_opt, double *tau);
+
+/* ------------------------------------------------------------------ */
 /* SRBD convex MPC: ConvexMpc + A1RobotControl::compute_grf            */
 /* ------------------------------------------------------------------ */
 #define QO_NX 13

@@ -68,6 +68,9 @@ SIGNATURES = {
     "qloco_rt_workspace_bytes": (C.c_int64, [i64]),
     "qloco_rt_init": (C.c_int, [i64, vp, vp]),
     "qloco_rt_tick": (C.c_int, [i64, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "qloco_servo_workspace_bytes": (C.c_int64, [i64]),
+    "qloco_servo_init": (C.c_int, [i64, vp, vp]),
+    "qloco_servo_force_block": (C.c_int, [C.POINTER(ForceParams), i64] + [vp] * 22),
 }
 
 

@@ -27,6 +27,7 @@ SOURCES = [
     "qloco_force.hip",
     "qloco_body.hip",
     "qloco_rt.hip",
+    "qloco_servo.hip",
     "qloco_gen.cpp",
 ]
 # per-file extra flags: the fp64 active-set kernel keeps the restatement's
@@ -38,7 +39,7 @@ SOURCES = [
 # loops are unrolled in full (static register per pivot column); the two-wave
 # inverse's body exceeds the default pragma-unroll budget, so it is raised.
 EXTRA = {"qloco_gi.hip": ["-ffp-contract=off"], "qloco_force.hip": ["-ffp-contract=off"],
-         "qloco_body.hip": ["-ffp-contract=off"], "qloco_rt.hip": ["-ffp-contract=off"], "qloco_kin.hip": ["-ffp-contract=off"], "qloco_srbd.hip": ["-fno-slp-vectorize", "-mllvm", "-pragma-unroll-threshold=200000"]}
+         "qloco_body.hip": ["-ffp-contract=off"], "qloco_rt.hip": ["-ffp-contract=off"], "qloco_servo.hip": ["-ffp-contract=off"], "qloco_kin.hip": ["-ffp-contract=off"], "qloco_srbd.hip": ["-fno-slp-vectorize", "-mllvm", "-pragma-unroll-threshold=200000"]}
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC]
 

@@ -135,3 +135,76 @@ def indexfind(t):
     check(lib().qloco_body_indexfind(t.shape[0], ptr(t.contiguous()), ptr(j), _stream(t)),
           "qloco_body_indexfind")
     return j
+
+
+class ServoForceBlock:
+    """The go1 servo loop's force block (servo.cpp:1052-1243, :1318) for B
+    robots: F_sum, rleg_com / F_lr_predict and the swing flags from the
+    desired motion, then force_distribution + force_opt and the four legs'
+    compute_joint_torques.  Member / loop state stays on the device."""
+
+    IN_F64 = ("coma_des", "com_des", "rfoot_des", "lfoot_des", "body_p_des", "foot_des")
+
+    def __init__(self, batch, device="cuda:0", **params):
+        import torch
+        self.batch = int(batch)
+        self.params = force_params(**params)
+        n = int(lib().qloco_servo_workspace_bytes(self.batch))
+        self.ws = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
+        f64 = dict(dtype=torch.float64, device=device)
+        i32 = dict(dtype=torch.int32, device=device)
+        self.out = {"F_sum": torch.zeros((batch, 6), **f64),
+                    "Force_L_R": torch.zeros((batch, 6), **f64),
+                    "grf_opt": torch.zeros((batch, 12), **f64),
+                    "tau": torch.zeros((batch, 12), **f64),
+                    "swing": torch.zeros((batch, 4), **i32),
+                    "qp_solution": torch.zeros(batch, **i32),
+                    "status": torch.zeros(batch, **i32)}
+        check(lib().qloco_servo_init(self.batch, ptr(self.ws), _stream(self.ws)), "qloco_servo_init")
+
+    def step(self, coma_des, com_des, rfoot_des, lfoot_des, body_p_des, foot_des, right_support,
+             gait_mode, y_offset, loop_count, Jaco, foot_rel_mea, v_est_rel):
+        o = self.out
+        check(lib().qloco_servo_force_block(
+            C.byref(self.params), self.batch, ptr(self.ws), ptr(coma_des), ptr(com_des),
+            ptr(rfoot_des), ptr(lfoot_des), ptr(body_p_des), ptr(foot_des), ptr(right_support),
+            ptr(gait_mode), ptr(y_offset), ptr(loop_count), ptr(Jaco), ptr(foot_rel_mea),
+            ptr(v_est_rel), ptr(o["F_sum"]), ptr(o["Force_L_R"]), ptr(o["grf_opt"]), ptr(o["tau"]),
+            ptr(o["swing"]), ptr(o["qp_solution"]), ptr(o["status"]), _stream(self.ws)),
+            "qloco_servo_force_block")
+        return o
+
+
+def synth_servo_inputs(seed, batch, tick):
+    """Deterministic servo-loop inputs for tick `tick` (numpy, legs FR, FL,
+    RR, RL): Go1 homing feet (servo.cpp:799-802) stepping with the body,
+    small desired COM accelerations, gait modes 101/102/103 and one outside
+    them (104, which keeps the swing flags), right_support cycling 0/1/2 on a
+    per-robot phase, FK-like Jacobians and measured feet near the desired."""
+    import numpy as np
+    rng = np.random.default_rng([seed, batch])
+    ph = rng.uniform(0, 2 * np.pi, batch)
+    mode = rng.choice([101, 102, 103, 104], batch, p=[0.3, 0.4, 0.2, 0.1]).astype(np.int32)
+    J0 = rng.normal(0, 0.15, (batch, 4, 3, 3)) + 0.3 * np.eye(3)
+    trng = np.random.default_rng([seed, batch, tick])
+    t = tick * 0.005
+    body = np.stack([0.05 * t + 0.01 * np.sin(ph), 0.02 * np.sin(3 * t + ph),
+                     0.30 + 0.005 * np.cos(5 * t + ph)], 1)
+    homing = np.array([[0.150786, -0.12675, 0.0], [0.150786, 0.12675, 0.0],
+                       [-0.225414, -0.12675, 0.0], [-0.225414, 0.12675, 0.0]])
+    feet = homing[None] + body[:, None, :] * np.array([1.0, 1.0, 0.0])
+    feet[:, :, 2] += 0.02 * np.maximum(np.sin(8 * t + ph[:, None] + np.arange(4)[None] * np.pi / 2), 0)
+    rs = ((np.floor(t / 0.35 + ph) % 3)).astype(np.int32)
+    rfoot = (feet[:, 0] + feet[:, 3]) / 2
+    lfoot = (feet[:, 1] + feet[:, 2]) / 2
+    com = body + trng.normal(0, 0.003, (batch, 3))
+    coma = trng.normal(0, 0.4, (batch, 3))
+    y = np.where(mode == 101, 0.75, np.where(mode == 102, 0.0, 0.11))
+    Jaco = J0 + 0.02 * np.sin(t + ph)[:, None, None, None]
+    rel_mea = (feet - body[:, None, :]) + trng.normal(0, 0.002, (batch, 4, 3))
+    v_est = trng.normal(0, 0.05, (batch, 4, 3))
+    return dict(coma_des=coma, com_des=com, rfoot_des=rfoot, lfoot_des=lfoot, body_p_des=body,
+                foot_des=feet.reshape(batch, 12), right_support=rs, gait_mode=mode, y_offset=y,
+                loop_count=np.full(batch, tick, np.int32),
+                Jaco=np.ascontiguousarray(np.transpose(Jaco, (0, 1, 3, 2))).reshape(batch, 36),
+                foot_rel_mea=rel_mea.reshape(batch, 12), v_est_rel=v_est.reshape(batch, 12))

@@ -151,6 +151,62 @@ def lib():
     return _lib
 
 
+class ServoState(C.Structure):
+    _fields_ = [("dyn", DynState), ("swing", C.c_int * 4), ("rel_des_old", C.c_double * 12),
+                ("v_rel", C.c_double * 12)]
+
+
+class ServoOracle:
+    """B go1 servo force blocks in the C restatement (oracle/servo_block.c)."""
+
+    def __init__(self, batch):
+        L = lib()
+        L.qo_servo_init.argtypes = [C.POINTER(ServoState)]
+        L.qo_servo_free.argtypes = [C.POINTER(ServoState)]
+        L.qo_servo_force_block.restype = C.c_int
+        L.qo_servo_force_block.argtypes = ([C.POINTER(ServoState), C.POINTER(ForceParams)] +
+                                           [dp] * 6 + [C.c_int, C.c_int, C.c_double, C.c_int] +
+                                           [dp] * 3 + [dp, dp, dp, dp, dp, ip, ip])
+        self.batch = batch
+        self.states = (ServoState * batch)()
+        for s in self.states:
+            L.qo_servo_init(C.byref(s))
+        self.prm = ForceParams()
+        L.qo_force_params_default(C.byref(self.prm))
+
+    def step(self, d):
+        B = self.batch
+        out = {"F_sum": np.zeros((B, 6)), "Force_L_R": np.zeros((B, 6)),
+               "grf_opt": np.zeros((B, 12)), "tau": np.zeros((B, 12)),
+               "swing": np.zeros((B, 4), np.int32), "qp_solution": np.zeros(B, np.int32),
+               "status": np.zeros(B, np.int32)}
+        row = lambda k, b: np.ascontiguousarray(d[k][b], np.float64)
+        for b in range(B):
+            sw = np.zeros(4, np.int32)
+            st = C.c_int(0)
+            ins = [row(k, b) for k in ("coma_des", "com_des", "rfoot_des", "lfoot_des",
+                                       "body_p_des", "foot_des")]
+            J, rm, ve = row("Jaco", b), row("foot_rel_mea", b), row("v_est_rel", b)
+            o = [np.zeros(6), np.zeros(6), np.zeros(12), np.zeros(12)]
+            ok = lib().qo_servo_force_block(
+                C.byref(self.states[b]), C.byref(self.prm), *[P(a) for a in ins],
+                int(d["right_support"][b]), int(d["gait_mode"][b]), float(d["y_offset"][b]),
+                int(d["loop_count"][b]), P(J), P(rm), P(ve), P(o[0]), P(o[1]), None, P(o[2]),
+                P(o[3]), sw.ctypes.data_as(ip), C.byref(st))
+            out["F_sum"][b], out["Force_L_R"][b], out["grf_opt"][b], out["tau"][b] = o
+            out["swing"][b], out["qp_solution"][b], out["status"][b] = sw, ok, st.value
+        return out
+
+    def __del__(self):
+        if getattr(self, "states", None) is not None and _lib is not None:
+            try:
+                for s in self.states:
+                    _lib.qo_servo_free(C.byref(s))
+            except Exception:
+                pass
+            self.states = None
+
+
 class RtOracle:
     """B rt_mpc_qp nodes in the C restatement (oracle/rt_tick.c)."""
     SCHED = 8
