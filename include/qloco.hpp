@@ -20,6 +20,7 @@
  *                                    ConvexMpc (A1RobotControl.cpp:452-600)
  *   Kinematicclass                <- go1_rt_control Kinematicclass
  *                                    (Kinematics.h:30-61; servo.cpp:734-741, :1038-1051)
+ *   ServoForceBlock               <- the go1 servo loop's force block (servo.cpp:1052-1243)
  *   RtMpcNode                     <- the rt_mpc_qp node loop (gait_fast.cpp:79-735):
  *                                    subscriber callbacks + one 100 Hz iteration
  *
@@ -277,6 +278,33 @@ class RtMpcNode {
   void *d_ws_;
   double *d_gait_, *d_ctrl_, *d_traj_, *d_nrt_;
   int32_t *d_sched_;
+};
+
+// ------------------------------------------------------------------------
+// The go1 servo loop's force block (servo.cpp:1052-1243, :1318) for B robots:
+// one call per servo tick replaces the F_sum / F_lr_predict / swing-flag
+// glue, Dynam.force_distribution + force_opt and the four
+// compute_joint_torques calls.  Host arrays of B consecutive records; legs
+// FR, FL, RR, RL; Jaco = the four Jacobian_kin (3x3 col-major) per robot.
+class ServoForceBlock {
+ public:
+  explicit ServoForceBlock(int batch = 1, const qloco_force_params *params = nullptr);
+  void step(const double *coma_des, const double *com_des, const double *rfoot_des,
+            const double *lfoot_des, const double *body_p_des, const double *foot_des,
+            const int32_t *right_support, const int32_t *gait_mode, const double *y_offset,
+            const int32_t *count_in_rt_loop, const double *Jaco, const double *foot_rel_mea,
+            const double *v_est_rel);
+  std::vector<double> F_sum, Force_L_R, grf_opt, Legs_torque;  // 6, 6, 12, 12 per robot
+  std::vector<int32_t> swing, qp_solution, status;             // 4, 1, 1 per robot
+  int batch() const { return batch_; }
+
+ private:
+  int batch_;
+  qloco_force_params prm_;
+  DeviceArena arena_;
+  void *d_ws_;
+  double *d_in_, *d_out_;
+  int32_t *d_iin_, *d_iout_;
 };
 
 }  // namespace qloco

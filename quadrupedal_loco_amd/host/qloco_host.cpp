@@ -599,4 +599,71 @@ void RtMpcNode::loop_once() {
   arena_.sync();
 }
 
+
+// ---------------------------------------------------------------- ServoForceBlock
+// double inputs, per robot: coma 3, com 3, rfoot 3, lfoot 3, body_p 3, foot 12,
+// y 1, Jaco 36, rel_mea 12, v_est 12 (= 88); int inputs: rs, mode, count (3);
+// double outputs: F_sum 6, FLR 6, grf 12, tau 12 (= 36); int outputs: swing 4, qps, status (6)
+ServoForceBlock::ServoForceBlock(int batch, const qloco_force_params *params) : batch_(batch) {
+  if (batch < 1) throw Error("ServoForceBlock: batch < 1", QLOCO_ERR_ARG);
+  if (params) prm_ = *params;
+  else qloco_force_params_default(&prm_);
+  const size_t B = batch;
+  F_sum.assign(B * 6, 0.0);
+  Force_L_R.assign(B * 6, 0.0);
+  grf_opt.assign(B * 12, 0.0);
+  Legs_torque.assign(B * 12, 0.0);
+  swing.assign(B * 4, 0);
+  qp_solution.assign(B, 1);
+  status.assign(B, 0);
+  const int64_t ws = qloco_servo_workspace_bytes(batch);
+  if (ws < 0) throw Error("qloco_servo_workspace_bytes", QLOCO_ERR_ARG);
+  d_ws_ = arena_.alloc((size_t)ws);
+  d_in_ = dalloc<double>(arena_, B * 88);
+  d_out_ = dalloc<double>(arena_, B * 36);
+  d_iin_ = dalloc<int32_t>(arena_, B * 3);
+  d_iout_ = dalloc<int32_t>(arena_, B * 6);
+  abi_ok(qloco_servo_init(batch, d_ws_, arena_.stream()), "qloco_servo_init");
+  arena_.sync();
+}
+
+void ServoForceBlock::step(const double *coma_des, const double *com_des, const double *rfoot_des,
+                           const double *lfoot_des, const double *body_p_des,
+                           const double *foot_des, const int32_t *right_support,
+                           const int32_t *gait_mode, const double *y_offset,
+                           const int32_t *count_in_rt_loop, const double *Jaco,
+                           const double *foot_rel_mea, const double *v_est_rel) {
+  const size_t B = batch_;
+  double *in = d_in_;
+  double *coma = in, *com = coma + 3 * B, *rf = com + 3 * B, *lf = rf + 3 * B, *bp = lf + 3 * B,
+         *ft = bp + 3 * B, *y = ft + 12 * B, *J = y + B, *rm = J + 36 * B, *ve = rm + 12 * B;
+  int32_t *rs = d_iin_, *md = rs + B, *cnt = md + B;
+  arena_.upload(coma, coma_des, sizeof(double) * 3 * B);
+  arena_.upload(com, com_des, sizeof(double) * 3 * B);
+  arena_.upload(rf, rfoot_des, sizeof(double) * 3 * B);
+  arena_.upload(lf, lfoot_des, sizeof(double) * 3 * B);
+  arena_.upload(bp, body_p_des, sizeof(double) * 3 * B);
+  arena_.upload(ft, foot_des, sizeof(double) * 12 * B);
+  arena_.upload(y, y_offset, sizeof(double) * B);
+  arena_.upload(J, Jaco, sizeof(double) * 36 * B);
+  arena_.upload(rm, foot_rel_mea, sizeof(double) * 12 * B);
+  arena_.upload(ve, v_est_rel, sizeof(double) * 12 * B);
+  arena_.upload(rs, right_support, sizeof(int32_t) * B);
+  arena_.upload(md, gait_mode, sizeof(int32_t) * B);
+  arena_.upload(cnt, count_in_rt_loop, sizeof(int32_t) * B);
+  double *Fs = d_out_, *Fl = Fs + 6 * B, *g = Fl + 6 * B, *tau = g + 12 * B;
+  int32_t *sw = d_iout_, *qps = sw + 4 * B, *st = qps + B;
+  abi_ok(qloco_servo_force_block(&prm_, batch_, d_ws_, coma, com, rf, lf, bp, ft, rs, md, y, cnt,
+                                 J, rm, ve, Fs, Fl, g, tau, sw, qps, st, arena_.stream()),
+         "qloco_servo_force_block");
+  arena_.download(F_sum.data(), Fs, sizeof(double) * 6 * B);
+  arena_.download(Force_L_R.data(), Fl, sizeof(double) * 6 * B);
+  arena_.download(grf_opt.data(), g, sizeof(double) * 12 * B);
+  arena_.download(Legs_torque.data(), tau, sizeof(double) * 12 * B);
+  arena_.download(swing.data(), sw, sizeof(int32_t) * 4 * B);
+  arena_.download(qp_solution.data(), qps, sizeof(int32_t) * B);
+  arena_.download(status.data(), st, sizeof(int32_t) * B);
+  arena_.sync();
+}
+
 }  // namespace qloco

@@ -11,6 +11,9 @@
 //  5. RtMpcNode (gait_fast.cpp loop) over 400 ticks of scripted messages vs
 //     qo_rt_tick_n: schedule integers and /rt2nrt/state bit-exact, /rtMPC/traj
 //     within 1e-9 (foot-rotation cos is the device libm's).
+//  6. ServoForceBlock (servo.cpp:1052-1243) over 40 ticks vs
+//     qo_servo_force_block: F_sum / F_lr_predict / swing bit-exact, grf_opt
+//     and torques within 1e-9.
 //  4. ConvexMpcBatch::compute_grf on the inputs of the reference harness
 //     test_mpc.cpp:18-91 (A1, mass 15, contacts FL, RL): forces within 0.5 N
 //     of the exact optimum committed in tests/golden/srbd_test_mpc_kat.npz.
@@ -311,6 +314,67 @@ static void test_rt_node() {
   std::printf("rt node ok: %d robots x %d ticks\n", B, T);
 }
 
+static void test_servo_block() {
+  const int B = 4, T = 40;
+  qloco::ServoForceBlock blk(B);
+  std::vector<qo_servo_state> ref(B);
+  for (auto &r : ref) qo_servo_init(&r);
+  qo_force_params prm;
+  qo_force_params_default(&prm);
+  const double homing[12] = {0.150786, -0.12675, 0, 0.150786, 0.12675, 0,
+                             -0.225414, -0.12675, 0, -0.225414, 0.12675, 0};
+  const int modes[B] = {101, 102, 103, 104};
+  std::vector<double> coma(3 * B), com(3 * B), rf(3 * B), lf(3 * B), bp(3 * B), ft(12 * B), y(B),
+      J(36 * B), rm(12 * B), ve(12 * B);
+  std::vector<int32_t> rs(B), md(B), cnt(B);
+  for (int t = 0; t < T; ++t) {
+    for (int b = 0; b < B; ++b) {
+      const double ph = 0.7 * b + 0.05 * t;
+      for (int k = 0; k < 3; ++k) coma[3 * b + k] = 0.3 * std::sin(ph + k);
+      bp[3 * b] = 0.01 * t;
+      bp[3 * b + 1] = 0.01 * std::sin(ph);
+      bp[3 * b + 2] = 0.3;
+      for (int k = 0; k < 12; ++k)
+        ft[12 * b + k] = homing[k] + (k % 3 == 2 ? 0.01 * std::fabs(std::sin(ph + k)) : bp[3 * b + k % 3]);
+      for (int k = 0; k < 3; ++k) {
+        com[3 * b + k] = bp[3 * b + k] + 0.002 * std::cos(ph + k);
+        rf[3 * b + k] = 0.5 * (ft[12 * b + k] + ft[12 * b + 9 + k]);
+        lf[3 * b + k] = 0.5 * (ft[12 * b + 3 + k] + ft[12 * b + 6 + k]);
+      }
+      for (int k = 0; k < 36; ++k) J[36 * b + k] = ((k % 4) == 0 ? 0.3 : 0.05 * std::sin(k + ph));
+      for (int k = 0; k < 12; ++k) {
+        rm[12 * b + k] = ft[12 * b + k] - bp[3 * b + k % 3] + 0.001 * std::cos(k + ph);
+        ve[12 * b + k] = 0.02 * std::sin(2 * k + ph);
+      }
+      md[b] = modes[b];
+      rs[b] = (t / 7 + b) % 3;
+      y[b] = md[b] == 101 ? 0.75 : (md[b] == 102 ? 0.0 : 0.11);
+      cnt[b] = t;
+    }
+    blk.step(coma.data(), com.data(), rf.data(), lf.data(), bp.data(), ft.data(), rs.data(),
+             md.data(), y.data(), cnt.data(), J.data(), rm.data(), ve.data());
+    for (int b = 0; b < B; ++b) {
+      double Fs[6], Fl[6], g[12], tau[12];
+      int sw[4], st = 0;
+      const int ok = qo_servo_force_block(&ref[b], &prm, &coma[3 * b], &com[3 * b], &rf[3 * b],
+                                          &lf[3 * b], &bp[3 * b], &ft[12 * b], rs[b], md[b], y[b],
+                                          cnt[b], &J[36 * b], &rm[12 * b], &ve[12 * b], Fs, Fl,
+                                          nullptr, g, tau, sw, &st);
+      for (int k = 0; k < 6; ++k)
+        CHECK(blk.F_sum[6 * b + k] == Fs[k] && blk.Force_L_R[6 * b + k] == Fl[k],
+              "servo F t=%d robot %d [%d]\n", t, b, k);
+      for (int k = 0; k < 4; ++k) CHECK(blk.swing[4 * b + k] == sw[k], "servo swing t=%d %d\n", t, b);
+      CHECK(blk.qp_solution[b] == ok && blk.status[b] == st, "servo status t=%d %d\n", t, b);
+      for (int k = 0; k < 12; ++k) {
+        CHECK(close(blk.grf_opt[12 * b + k], g[k], 1e-9, 1e-8), "servo grf t=%d %d [%d]\n", t, b, k);
+        CHECK(close(blk.Legs_torque[12 * b + k], tau[k], 1e-9, 1e-9), "servo tau t=%d %d [%d]\n", t, b, k);
+      }
+    }
+  }
+  for (auto &r : ref) qo_servo_free(&r);
+  std::printf("servo force block ok: %d robots x %d ticks\n", B, T);
+}
+
 int main() {
   try {
     test_force_qp();
@@ -319,6 +383,7 @@ int main() {
     test_convex_mpc();
     test_kinematics();
     test_rt_node();
+    test_servo_block();
   } catch (const qloco::Error &e) {
     std::printf("FAIL: qloco::Error %s (status %d)\n", e.what(), e.status);
     return 2;
