@@ -116,7 +116,10 @@ __device__ void force_distribution(const double *com_des, const double *leg_des,
 #undef FRC
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void force_qp_kernel(
+#ifndef QLOCO_FORCE_WPE  // waves per SIMD the register budget targets
+#define QLOCO_FORCE_WPE 2
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_WPE))) void force_qp_kernel(
     const ForceArgs a) {
   __shared__ ForceLds S;
   const int lane = threadIdx.x, grp = lane >> 4, li = lane & 15;
