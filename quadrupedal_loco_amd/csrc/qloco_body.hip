@@ -127,11 +127,13 @@ struct BodyArgs {
   double *state, *com_traj;
   int *status;
   // rt node tick (qloco_rt.hip): the robot's own _tx (Foot_trajectory_solve_mod2
-  // rewrites it, PRMPCClass.cpp:1773-1779) at tx[j * tx_stride + inst], and a
-  // mask of the robots whose loop calls body_theta_mpc this tick.  NULL: the
-  // Initialize() schedule for every instance / all run.
+  // rewrites it, PRMPCClass.cpp:1773-1779) at tx[j * tx_stride + inst] or,
+  // with tx_tile > 0 (the rt workspace's 64-robot tiles), at
+  // tx[(inst / 64) * tx_tile + j * tx_stride + inst % 64], and a mask of the
+  // robots whose loop calls body_theta_mpc this tick.  NULL: the Initialize()
+  // schedule for every instance / all run.
   const double *tx;
-  int64_t tx_stride;
+  int64_t tx_stride, tx_tile;
   const int32_t *run;
   // row stride (doubles) of the reference arrays: 0 = packed (4 / 10 / 15);
   // the rt tick keeps all of a robot's references in one 64-double record
@@ -198,8 +200,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
   if (active) {
     const double t_f0 = (i + 1) * K.dt_mpc, t_f3 = (i + BNH) * K.dt_mpc;  // :406
     if (a.tx) {
-      bjx1 = indexfind(a.tx + inst, a.tx_stride, t_f0) + 1;
-      bjx2 = indexfind(a.tx + inst, a.tx_stride, t_f3) + 1;
+      const double *txr = a.tx + (a.tx_tile > 0 ? (inst >> 6) * a.tx_tile + (inst & 63) : inst);
+      bjx1 = indexfind(txr, a.tx_stride, t_f0) + 1;
+      bjx2 = indexfind(txr, a.tx_stride, t_f3) + 1;
     } else {
       bjx1 = indexfind(K, t_f0) + 1;
       bjx2 = indexfind(K, t_f3) + 1;
@@ -361,7 +364,7 @@ int body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyangle_sta
                     const double *zmp_ref, const double *angle_ref, const double *rfoot_ref,
                     const double *lfoot_ref, const double *comacc_ref, double *state,
                     double *com_traj, int32_t *status, const double *tx, int64_t tx_stride,
-                    const int32_t *run, int64_t ref_ld, hipStream_t stream);
+                    int64_t tx_tile, const int32_t *run, int64_t ref_ld, hipStream_t stream);
 
 __global__ void indexfind_kernel(const BodyConsts k, int64_t batch, const double *t, int *j) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -391,7 +394,7 @@ extern "C" int qloco_body_mpc_step(int64_t batch, const int32_t *i,
       !comacc_ref || !state || !com_traj)
     return QLOCO_ERR_ARG;
   return body_mpc_launch(batch, i, bodyangle_state, zmp_ref, angle_ref, rfoot_ref, lfoot_ref,
-                         comacc_ref, state, com_traj, status, nullptr, 0, nullptr, 0,
+                         comacc_ref, state, com_traj, status, nullptr, 0, 0, nullptr, 0,
                          (hipStream_t)stream);
 }
 
@@ -429,7 +432,8 @@ int qloco::body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyan
                            const double *rfoot_ref, const double *lfoot_ref,
                            const double *comacc_ref, double *state, double *com_traj,
                            int32_t *status, const double *tx, int64_t tx_stride,
-                           const int32_t *run, int64_t ref_ld, hipStream_t stream) {
+                           int64_t tx_tile, const int32_t *run, int64_t ref_ld,
+                           hipStream_t stream) {
   BodyArgs a;
   memset(&a, 0, sizeof(a));
   body_constants(a.k);
@@ -446,6 +450,7 @@ int qloco::body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyan
   a.status = status;
   a.tx = tx;
   a.tx_stride = tx_stride;
+  a.tx_tile = tx_tile;
   a.run = run;
   a.ref_ld = ref_ld;
   const int rc = body_ci_upload(a.k);

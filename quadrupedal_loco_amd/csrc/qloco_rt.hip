@@ -19,9 +19,12 @@
 //                    each robot's own _tx schedule
 //   rt_post_kernel   one robot per lane: packs /rtMPC/traj, /rt2nrt/state
 //
-// State lives in one device workspace: the node/generator members
-// field-major (SoA: field f of robot r at d[f*B + r], so every lane access of
-// a field is one coalesced 512-byte row per wave), the body-MPC records
+// State lives in one device workspace: the node/generator members in
+// 64-robot tiles, field-major inside a tile (field f of robot r at
+// d[(r / 64) * F_DOUBLES * 64 + f * 64 + r % 64]: every lane access of a
+// field is one coalesced 512-byte row per wave, and the field offsets are
+// compile-time constants, so the compiler can tell fields apart and batch
+// loads across the stores of other fields), the body-MPC records
 // (QLOCO_BODY_STATE_LEN doubles per robot, shared with qloco_body_mpc_step)
 // and per-tick scratch.  fp64 throughout, compiled without FMA contraction
 // so the schedule arithmetic follows the restatement (oracle/rt_tick.c)
@@ -42,7 +45,7 @@ int body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyangle_sta
                     const double *zmp_ref, const double *angle_ref, const double *rfoot_ref,
                     const double *lfoot_ref, const double *comacc_ref, double *state,
                     double *com_traj, int32_t *status, const double *tx, int64_t tx_stride,
-                    const int32_t *run, int64_t ref_ld, hipStream_t stream);
+                    int64_t tx_tile, const int32_t *run, int64_t ref_ld, hipStream_t stream);
 
 namespace rt {
 
@@ -86,15 +89,17 @@ enum { RX = 0, RY, RZ, RVX, RVY, RVZ, RAX, RAY, RAZ, LX, LY, LZ, LVX, LVY, LVZ, 
 // col-major), comacc_mpc_ref (3x5)
 enum : int { RF_BAS = 0, RF_ZMP = 4, RF_ANG = 14, RF_RFT = 24, RF_LFT = 34, RF_ACC = 44,
              RF_USED = 59, RF_LD = 64 };
+constexpr int TL = 64;  // robots per state tile (one wave)
 struct Ws {  // byte offsets into the workspace
   int64_t d, n, body, ref, ct, bi, run, st, total;
 };
 __host__ __device__ inline Ws layout(int64_t B) {
   Ws w;
   auto al = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+  const int64_t Bt = (B + TL - 1) / TL * TL;  // whole tiles
   w.d = 0;
-  w.n = al(w.d + 8 * F_DOUBLES * B);
-  w.body = al(w.n + 4 * I_INTS * B);
+  w.n = al(w.d + 8 * F_DOUBLES * Bt);
+  w.body = al(w.n + 4 * I_INTS * Bt);
   w.ref = al(w.body + 8 * QLOCO_BODY_STATE_LEN * B);
   w.ct = al(w.ref + 8 * RF_LD * B);
   w.bi = al(w.ct + 8 * 14 * B);
@@ -113,13 +118,15 @@ struct RtArgs {
   double aaa_inv_mod[16];  // solve_AAA_inv_mod1 (:1344-1362), col-major
 };
 
-// per-lane view of one robot's SoA state
+// per-lane view of one robot's tiled state
 struct Robot {
   double *__restrict__ d;
   int32_t *__restrict__ n;
-  int64_t B;
-  __device__ double &D(int f) const { return d[(int64_t)f * B]; }
-  __device__ int32_t &I(int f) const { return n[(int64_t)f * B]; }
+  __device__ Robot(char *ws, const Ws &L, int64_t r)
+      : d(reinterpret_cast<double *>(ws + L.d) + (r / TL) * (F_DOUBLES * TL) + r % TL),
+        n(reinterpret_cast<int32_t *>(ws + L.n) + (r / TL) * (I_INTS * TL) + r % TL) {}
+  __device__ double &D(int f) const { return d[f * TL]; }
+  __device__ int32_t &I(int f) const { return n[f * TL]; }
   __device__ double &foot(int a, int k) const { return D(F_FOOT + a * 6 + k); }
   __device__ double &fxyz(int a, int i) const { return D(F_FXYZ + a * NS + i); }
 };
@@ -560,7 +567,7 @@ __global__ __launch_bounds__(PRE_T) void rt_pre_kernel(const RtArgs a) {
   const int64_t r = r0 + tid;
   const bool live = tid < nb;
   const Ws L = layout(B);
-  Robot R{reinterpret_cast<double *>(a.ws + L.d) + r, reinterpret_cast<int32_t *>(a.ws + L.n) + r, B};
+  Robot R(a.ws, L, r);
   const double *ctrl = a.ctrl + r * QLOCO_CTRL_MSG_LEN;
   int do_body = 0;
   if (live) {
@@ -647,7 +654,7 @@ __global__ __launch_bounds__(POST_T) void rt_post_kernel(const RtArgs a) {
   const int64_t r = r0 + tid;
   const bool live = tid < nb;
   const Ws L = layout(B);
-  Robot R{reinterpret_cast<double *>(a.ws + L.d) + r, reinterpret_cast<int32_t *>(a.ws + L.n) + r, B};
+  Robot R(a.ws, L, r);
   const double *body = reinterpret_cast<const double *>(a.ws + L.body) + r * QLOCO_BODY_STATE_LEN;
   const double *g = a.gait + r * QLOCO_GAIT_MSG_LEN;
   // [0, 36): the /MPC/Gait rows copied through (:716-719)
@@ -684,7 +691,7 @@ __global__ __launch_bounds__(256) void rt_init_kernel(int64_t B, char *ws) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= B) return;
   const Ws L = layout(B);
-  Robot R{reinterpret_cast<double *>(ws + L.d) + r, reinterpret_cast<int32_t *>(ws + L.n) + r, B};
+  Robot R(ws, L, r);
   for (int f = 0; f < F_DOUBLES; ++f) R.D(f) = 0.0;
   for (int f = 0; f < I_INTS; ++f) R.I(f) = 0;
   double *body = reinterpret_cast<double *>(ws + L.body) + r * QLOCO_BODY_STATE_LEN;
@@ -783,7 +790,7 @@ extern "C" int qloco_rt_tick(int64_t batch, void *workspace, const double *gait_
       (const double *)(w + L.ref) + rt::RF_RFT, (const double *)(w + L.ref) + rt::RF_LFT,
       (const double *)(w + L.ref) + rt::RF_ACC, (double *)(w + L.body),
       (double *)(w + L.ct), (int32_t *)(w + L.st),
-      (const double *)(w + L.d) + (int64_t)rt::F_TX * batch, batch,
+      (const double *)(w + L.d) + rt::F_TX * rt::TL, rt::TL, rt::F_DOUBLES * rt::TL,
       (const int32_t *)(w + L.run), rt::RF_LD, s);
   if (rc != QLOCO_OK) return rc;
   hipLaunchKernelGGL(rt::rt_post_kernel, dim3((unsigned)((batch + rt::POST_T - 1) / rt::POST_T)),
