@@ -308,6 +308,23 @@ int qloco_servo_force_block(const qloco_force_params *prm, int64_t batch, void *
                             double *grf_opt, double *tau, int32_t *swing,
                             int32_t *qp_solution, int32_t *status, void *stream);
 
+/* ====================================================================== */
+/* 8. slow planner's contact-phase flag, batched     */
+/*    replaces the schedule indices of NLPClass::step_timing_opti_loop     */
+/*    (mosek_nlp_kmp NLPClass_sqp.cpp:1029-1039) and the right_support     */
+/*    branch of NLPClass::Foot_trajectory_solve_mod2 (:2076-2090,          */
+/*    :2187-2202, :2311-2313) -- the /MPC/Gait[99] flag servo.cpp:673 reads */
+/* ====================================================================== */
+/* ts[B*27], tx[B*27] (device, double): each robot's _ts / _tx after the
+ * planner's step-timing update (row per robot); t_int[B] (_t_int, the slow
+ * loop index) and t_end_footstep[B] (int32).  Outputs (int32): bjxx[B] and
+ * bjx1[B] (optional), right_support[B] (0 left, 1 right, 2 double
+ * support).  Integer results are bit-exact with the restatement. */
+#define QLOCO_NLP_STEPS 27
+int qloco_support_phase(int64_t batch, const double *ts, const double *tx, const int32_t *t_int,
+                        const int32_t *t_end_footstep, int32_t *bjxx, int32_t *bjx1,
+                        int32_t *right_support, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

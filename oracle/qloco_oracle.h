@@ -305,6 +305,15 @@ void qo_leg_ik_batch(int64_t n, const double *pos_des, const double *q_ini, cons
                      const double *body_p, const double *body_r, double *q, double *pos, double *J,
                      int32_t *updates);
 
+/* ------------------------------------------------------------------ */
+/* Slow planner's contact-phase flag (support_phase.c): NLPClass_sqp.cpp */
+/* :1029-1039 schedule indices + Foot_trajectory_solve_mod2 right_support */
+/* ------------------------------------------------------------------ */
+/* ts, tx: n x 27 (row per robot); t_int, t_end_footstep: n.  Outputs n. */
+void qo_support_phase(int64_t n, const double *ts, const double *tx, const int32_t *t_int,
+                      const int32_t *t_end_footstep, int32_t *bjxx, int32_t *bjx1,
+                      int32_t *right_support);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,6 +71,7 @@ SIGNATURES = {
     "qloco_servo_workspace_bytes": (C.c_int64, [i64]),
     "qloco_servo_init": (C.c_int, [i64, vp, vp]),
     "qloco_servo_force_block": (C.c_int, [C.POINTER(ForceParams), i64] + [vp] * 22),
+    "qloco_support_phase": (C.c_int, [i64] + [vp] * 8),
 }
 
 

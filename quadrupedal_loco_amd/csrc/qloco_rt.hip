@@ -727,6 +727,79 @@ __global__ __launch_bounds__(256) void rt_init_kernel(int64_t B, char *ws) {
   }
 }
 
+// Slow planner's contact-phase flag (mosek_nlp_kmp NLPClass; oracle/
+// support_phase.c): bjxx / bjx1 from the planner's own _tx after its
+// step-timing SQP (NLPClass_sqp.cpp:1029-1039, Indexfind :1105-1142 with
+// xyz1, bounded at 27) and Foot_trajectory_solve_mod2's right_support
+// (:2076-2090, :2187-2202, :2311-2313).  64 robots per block: the block's
+// _ts / _tx rows (27 doubles each, contiguous for consecutive robots) are
+// staged through LDS by all 256 threads with coalesced 16-byte loads (a
+// 64-robot row block is 13.8 KB, 16-byte aligned), then one lane per robot
+// runs the scan out of LDS.
+constexpr int SP_T = 64;    // robots per block
+constexpr int SP_TH = 256;  // threads per block: 4 per robot for the row loads
+constexpr double SP_DT = 0.025;  // NLPClass.h:32
+__global__ __launch_bounds__(SP_TH) void support_phase_kernel(int64_t B, const double *ts,
+                                                              const double *tx,
+                                                              const int32_t *t_int,
+                                                              const int32_t *t_end,
+                                                              int32_t *bjxx, int32_t *bjx1,
+                                                              int32_t *rs) {
+  __shared__ __attribute__((aligned(16))) double sts[SP_T * NS], stx[SP_T * NS];
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * SP_T;
+  const int nb = (int)((B - r0) < SP_T ? (B - r0) : SP_T);
+  if (nb == SP_T) {  // whole block: 16-byte loads, all issued before the LDS stores
+    constexpr int NV = SP_T * NS / 2, PER = (NV + SP_TH - 1) / SP_TH;
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v *gs = reinterpret_cast<const d2v *>(ts + r0 * NS);
+    const d2v *gx = reinterpret_cast<const d2v *>(tx + r0 * NS);
+    d2v vs[PER], vx[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int k = tid + q * SP_TH;
+      if (k < NV) {
+        vs[q] = __builtin_nontemporal_load(gs + k);
+        vx[q] = __builtin_nontemporal_load(gx + k);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int k = tid + q * SP_TH;
+      if (k < NV) {
+        reinterpret_cast<d2v *>(sts)[k] = vs[q];
+        reinterpret_cast<d2v *>(stx)[k] = vx[q];
+      }
+    }
+  } else {
+    for (int k = tid; k < nb * NS; k += SP_TH) {
+      sts[k] = ts[r0 * NS + k];
+      stx[k] = tx[r0 * NS + k];
+    }
+  }
+  __syncthreads();
+  if (tid >= nb) return;
+  const int64_t r = r0 + tid;
+  const double *x = stx + tid * NS;
+  const int i = t_int[r];
+  auto find = [&](double goal) {
+    int j = 0;
+    while (j < NS && goal >= x[j]) j++;
+    return j - 1;
+  };
+  const int bxx = find(i * SP_DT) + 1;
+  const int b1 = find((i + 1) * SP_DT) + 1;
+  int f = 2;
+  if (b1 >= 2 && i <= t_end[r]) {
+    const double td = 0.2 * sts[tid * NS + b1 - 1];
+    f = (b1 % 2 == 0) ? 0 : 1;
+    if ((i + 1 - round(x[b1 - 1] / SP_DT)) * SP_DT < td) f = 2;
+  }
+  if (bjxx) bjxx[r] = bxx;
+  if (bjx1) bjx1[r] = b1;
+  rs[r] = f;
+}
+
 static void aaa_inv_mod(double out[16]) {  // :1344-1362
   const double t[4] = {-DT_SLOW, 0, DT_SLOW, 2 * DT_SLOW};
   double A[16], Ai[16];
@@ -796,5 +869,21 @@ extern "C" int qloco_rt_tick(int64_t batch, void *workspace, const double *gait_
   hipLaunchKernelGGL(rt::rt_post_kernel, dim3((unsigned)((batch + rt::POST_T - 1) / rt::POST_T)),
                      dim3(rt::POST_T), 0, s, a);
   QLOCO_HIP_CHECK(hipGetLastError(), "rt_post_kernel launch");
+  return QLOCO_OK;
+}
+
+extern "C" int qloco_support_phase(int64_t batch, const double *ts, const double *tx,
+                                   const int32_t *t_int, const int32_t *t_end_footstep,
+                                   int32_t *bjxx, int32_t *bjx1, int32_t *right_support,
+                                   void *stream) {
+  if (batch < 0) return QLOCO_ERR_ARG;
+  if (batch == 0) return QLOCO_OK;
+  if (!ts || !tx || !t_int || !t_end_footstep || !right_support) return QLOCO_ERR_ARG;
+  if (batch > (int64_t)0x7fffffff * rt::SP_T) return QLOCO_BAD_SIZE;
+  hipLaunchKernelGGL(rt::support_phase_kernel,
+                     dim3((unsigned)((batch + rt::SP_T - 1) / rt::SP_T)), dim3(rt::SP_TH), 0,
+                     (hipStream_t)stream, batch, ts, tx, t_int, t_end_footstep, bjxx, bjx1,
+                     right_support);
+  QLOCO_HIP_CHECK(hipGetLastError(), "support_phase_kernel launch");
   return QLOCO_OK;
 }

@@ -1052,7 +1052,16 @@ void srbd_admm_kernel(const SrbdArgs a) {
         float xt;
         {
           const f4v r0 = S.bc[buf][lane & 15];
-          if constexpr (W == 1) {  // two accumulator chains
+          if constexpr (W == 1) {
+#ifdef QLOCO_MATVEC4  // four accumulator chains
+            float acc0, acc1, acc2, acc3;
+            if constexpr (C60) {
+              QL_DPP_MATVEC60(acc0, acc1, acc2, acc3, r0, K.k, 0);
+            } else {
+              QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r0, K.k, 0);
+            }
+            xt = (acc0 + acc1) + (acc2 + acc3);
+#else  // two accumulator chains
             float acc0, acc1;
             if constexpr (C60) {
               QL_DPP_MATVEC60_2(acc0, acc1, r0, K.k, 0);
@@ -1060,6 +1069,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
               QL_DPP_MATVEC64_2(acc0, acc1, r0, K.k, 0);
             }
             xt = acc0 + acc1;
+#endif
           } else {
             float acc0, acc1, acc2, acc3;
             QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r0, K.k, 0);

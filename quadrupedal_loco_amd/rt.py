@@ -158,3 +158,58 @@ def synth_messages(seed, batch, tick, first=0):
     right_support = np.where(bjxx < 2, 2, bjxx % 2)
     gait[99] = np.where(counter_flag, m + 1, right_support)
     return np.ascontiguousarray(gait.T), np.ascontiguousarray(ctrl.T)
+
+
+NLP_STEPS, NLP_DT = 27, 0.025  # NLPClass _footstepsnumber, _dt (NLPClass.h:32)
+
+
+def support_phase(ts, tx, t_int, t_end_footstep, stream=None):
+    """Slow planner's contact-phase flag for B robots (qloco_support_phase):
+    ts, tx (B, 27) float64, t_int, t_end_footstep (B,) int32 device tensors
+    -> (bjxx, bjx1, right_support) int32 device tensors.  Restates
+    NLPClass_sqp.cpp:1029-1039 + Foot_trajectory_solve_mod2's right_support
+    (mosek_nlp_kmp); right_support is what /MPC/Gait[99] carries to servo.cpp:673."""
+    import torch
+    B = int(t_int.shape[0])
+    for name, t, shape, dt in (("ts", ts, (B, NLP_STEPS), torch.float64),
+                               ("tx", tx, (B, NLP_STEPS), torch.float64),
+                               ("t_int", t_int, (B,), torch.int32),
+                               ("t_end_footstep", t_end_footstep, (B,), torch.int32)):
+        if tuple(t.shape) != shape or t.dtype != dt or not t.is_contiguous() or not t.is_cuda:
+            raise ValueError("%s: expected contiguous %s %s on the GPU" % (name, shape, dt))
+    out = torch.empty((3, B), dtype=torch.int32, device=t_int.device)
+    s = _stream(t_int) if stream is None else stream
+    check(lib().qloco_support_phase(B, ptr(ts), ptr(tx), ptr(t_int), ptr(t_end_footstep),
+                                    ptr(out[0]), ptr(out[1]), ptr(out[2]), s),
+          "qloco_support_phase")
+    return out[0], out[1], out[2]
+
+
+def synth_schedules(seed, batch):
+    """Deterministic planner schedules (numpy): per robot a current step k,
+    _ts = 0.7 s (Initialize) up to k and SQP-updated durations in [0.45, 1.0]
+    after it; _tx rounded to the 0.025 s grid minus 1e-6 up to k
+    (NLPClass_sqp.cpp:204-205) and accumulated unrounded after it (:908);
+    t_int inside or around step k (a quarter exactly on the grid points of
+    _tx), t_end_footstep = round((_tx(26) - 2 * 0.7) / dt) (:593) with some
+    robots past it.  Returns ts, tx (B, 27) f64 and t_int, t_end (B,) i32."""
+    rng = np.random.default_rng(seed)
+    B, S, dt = batch, NLP_STEPS, NLP_DT
+    k = rng.integers(1, S - 1, size=B)
+    ts = np.full((B, S), 0.7)
+    upd = np.arange(S)[None, :] >= k[:, None]
+    ts = np.where(upd, rng.uniform(0.45, 1.0, size=(B, S)), ts)
+    tx = np.zeros((B, S))
+    for i in range(1, S):
+        rounded = np.round((tx[:, i - 1] + ts[:, i - 1]) / dt) * dt - 0.000001
+        tx[:, i] = np.where(i <= k, rounded, tx[:, i - 1] + ts[:, i - 1])
+    lo = np.round(tx[np.arange(B), k - 1] / dt).astype(np.int64)
+    hi = np.round(tx[np.arange(B), k] / dt).astype(np.int64)
+    t_int = lo + (rng.uniform(size=B) * (hi - lo + 6)).astype(np.int64) - 3
+    on_grid = rng.uniform(size=B) < 0.25
+    t_int = np.where(on_grid, lo, t_int)
+    t_int = np.maximum(t_int, 0)
+    t_end = np.round((tx[:, S - 1] - 2 * 0.7) / dt).astype(np.int64)
+    late = rng.uniform(size=B) < 0.1
+    t_end = np.where(late, t_int - 1 - rng.integers(0, 5, size=B), t_end)
+    return ts, tx, t_int.astype(np.int32), t_end.astype(np.int32)

@@ -147,6 +147,7 @@ def lib():
         L.qo_rt_destroy_n.argtypes = [C.c_void_p, C.c_int64]
         L.qo_rt_tick_n.argtypes = [C.c_void_p, C.c_int64] + [C.c_void_p] * 6
         L.qo_inv4.argtypes = [dp, dp]
+        L.qo_support_phase.argtypes = [C.c_int64] + [C.c_void_p] * 7
         _lib = L
     return _lib
 
@@ -377,3 +378,17 @@ def leg_ik(pos_des, q_ini, flag, body_p=None, body_r=None):
     n = lib().qo_leg_ik(bp, br, P(np.ascontiguousarray(pos_des, np.float64)),
                         P(np.ascontiguousarray(q_ini, np.float64)), int(flag), P(q), P(pos), P(J))
     return q, pos, J, n
+
+
+def support_phase(ts, tx, t_int, t_end):
+    """oracle/support_phase.c over numpy arrays -> (bjxx, bjx1, right_support)"""
+    ts = np.ascontiguousarray(ts, np.float64)
+    tx = np.ascontiguousarray(tx, np.float64)
+    t_int = np.ascontiguousarray(t_int, np.int32)
+    t_end = np.ascontiguousarray(t_end, np.int32)
+    n = t_int.shape[0]
+    out = np.zeros((3, n), np.int32)
+    lib().qo_support_phase(n, ts.ctypes.data, tx.ctypes.data, t_int.ctypes.data,
+                           t_end.ctypes.data, out[0].ctypes.data, out[1].ctypes.data,
+                           out[2].ctypes.data)
+    return out[0], out[1], out[2]

@@ -23,6 +23,13 @@ record 32 = 335 doubles + 7 ints) = 4728 B -> 6728 B per robot-tick.
 Peak 8.0 TB/s (MI355X_MICROARCH.md).  `traffic` = measured HBM bytes per
 tick (profiles/traffic_rt_tick_b65536.json, FETCH_SIZE / WRITE_SIZE passes).
 cpu_baseline: oracle/rt_tick.c (qo_rt_tick_n), 1 thread, bounded sample.
+
+    python tools/bench_rt.py --support [--robots B]
+
+measures the slow planner's contact-phase flag instead (qloco_support_phase,
+SURVEY.md §8f row 2): default 4M robots, algorithmic bytes per robot
+_ts + _tx rows 2 x 27 x 8 + t_int, t_end 8 + bjxx, bjx1, right_support 12 =
+452 B; cpu_baseline oracle/support_phase.c, 1 thread.
 """
 import argparse
 import json
@@ -69,6 +76,62 @@ def cpu_baseline(sets, budget_s=8.0):
     return n * ticks / dt, "%d robots x %d ticks (after 150 warm-up ticks)" % (n, ticks)
 
 
+SUPPORT_BYTES = 2 * 27 * 8 + 8 + 12
+
+
+def _support_traffic(B):
+    """measured HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) if profiled at this B"""
+    f = os.path.join(ROOT, "profiles", "traffic_support_phase_b%d.json" % B)
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        return json.load(fh).get("hbm_bytes_per_launch")
+
+
+def bench_support(args):
+    import torch
+    from quadrupedal_loco_amd.rt import support_phase, synth_schedules
+    B = args.robots if args.robots != 65536 else 1 << 22
+    dev = torch.device("cuda:0")
+    host = synth_schedules(SEED, B)
+    arrs = [torch.from_numpy(a).to(dev) for a in host]
+    for _ in range(args.warmup if args.warmup != 150 else 5):
+        support_phase(*arrs)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    ev[0].record(stream)
+    for k in range(args.steps):
+        support_phase(*arrs)
+        ev[k + 1].record(stream)
+    torch.cuda.synchronize()
+    per = np.array([ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)])
+    ms = float(per.mean())
+    achieved = SUPPORT_BYTES * B / (ms * 1e-3) / 1e9
+    line = {"metric": "NLP contact-phase flags/sec (NLPClass schedule indices + right_support)",
+            "value": B / (ms * 1e-3), "unit": "robots/s", "n_gpus": 1, "steps": args.steps,
+            "ms_per_step": ms, "higher_is_better": True, "dtype": "f64",
+            "data": "synthetic planner schedules (quadrupedal_loco_amd.rt.synth_schedules)",
+            "config": {"workload": "support phase, %d robots" % B},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_robot": SUPPORT_BYTES,
+                         "traffic": _support_traffic(B)}}
+    if not args.no_cpu_baseline:
+        import oracle_lib as O
+        n = 1 << 20
+        sub = [a[:n] for a in host]
+        t0, reps = time.perf_counter(), 0
+        while time.perf_counter() - t0 < 5.0:
+            O.support_phase(*sub)
+            reps += 1
+        dt = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": n * reps / dt, "unit": "robots/s", "cores": 1,
+                                "kind": "port", "sample": "%d x %d robots, oracle/support_phase.c"
+                                % (reps, n)}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--robots", type=int, default=65536)
@@ -76,7 +139,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=150)
     ap.add_argument("--sets", type=int, default=40)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--support", action="store_true")
     args = ap.parse_args()
+    if args.support:
+        return bench_support(args)
     import torch
     from quadrupedal_loco_amd.rt import RtNodeBatch, synth_messages
     B, M = args.robots, args.sets

@@ -118,5 +118,7 @@ if __name__ == "__main__":
                 gj(15) + "\n" + mul(15) + "\n" + absmax(15) + "\n" + matvec2(15) + "\n" +
                 # W = 2 second-half forms (columns 64.. of the row): 60 and 36 columns
                 matvec(True, 15) + "\n" + matvec(True, 9) + "\n" + gj(9) + "\n" + mul(9) + "\n" +
-                absmax(9))
+                absmax(9) + "\n" +
+                # four-chain 60-column form (W = 1, QLOCO_MATVEC4)
+                matvec(False, 15))
     print(OUT)
