@@ -32,6 +32,16 @@ HBM_PEAK_GBS = 8000.0
 BYTES = {"fk": 172, "ik": 224}
 
 
+def _traffic(kind, n):
+    """measured HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, separate
+    rocprofv3 passes) when profiled at this size (profiles/traffic_leg_*_4m.json)"""
+    f = os.path.join(ROOT, "profiles", "traffic_leg_%s_4m.json" % kind)
+    if n != 1 << 22 or not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        return json.load(fh).get("hbm_bytes_per_launch")
+
+
 def inputs(n, seed=11):
     rng = np.random.default_rng(seed)
     q = np.stack([rng.uniform(-0.5, 0.5, n), rng.uniform(0.4, 1.4, n), rng.uniform(-2.2, -1.0, n)], 1)
@@ -106,7 +116,8 @@ def main():
                 "config": {"workload": "%s, %d legs (%d robots x 4)" % (kind, n, n // 4)},
                 "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                             "algorithmic_bytes_per_leg": BYTES[kind], "traffic": None}}
+                             "algorithmic_bytes_per_leg": BYTES[kind],
+                             "traffic": _traffic(kind, n)}}
         if kind == "ik":
             upd = out[3]
             line["newton_updates_mean"] = float(upd.float().mean().item())
