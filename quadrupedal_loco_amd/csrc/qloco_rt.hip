@@ -269,10 +269,12 @@ __device__ void position_mod3(const RtArgs &a, const Robot &R, int walktime, int
   }
 }
 
-// one swing-foot axis (:1903-1951 right / :2069-2118 left)
-__device__ __forceinline__ void swing_axis(const Robot &R, const double Ai[16], double t_des,
-                                           int p, int v, int acc, int k, double mid, double end) {
-  const double plan[4] = {R.foot(p, k - 1), mid, end, 0};
+// one swing-foot axis (:1903-1951 right / :2069-2118 left): the cubic
+// through (start, mid, end) and zero end velocity, evaluated at t_des
+__device__ __forceinline__ void swing_axis(const double Ai[16], double t_des, double start,
+                                           double mid, double end, double &xp, double &xv,
+                                           double &xa) {
+  const double plan[4] = {start, mid, end, 0};
   double co[4];
   for (int r = 0; r < 4; ++r) {
     double s = 0;
@@ -282,15 +284,14 @@ __device__ __forceinline__ void swing_axis(const Robot &R, const double Ai[16], 
   const double tp[4] = {cube(t_des), sq(t_des), (t_des), 1};
   const double tv[4] = {3 * sq(t_des), 2 * (t_des), 1, 0};
   const double ta[4] = {6 * (t_des), 2, 0, 0};
-  double xp = 0, xv = 0, xa = 0;
+  xp = 0;
+  xv = 0;
+  xa = 0;
   for (int c = 0; c < 4; ++c) {
     xp += tp[c] * co[c];
     xv += tv[c] * co[c];
     xa += ta[c] * co[c];
   }
-  R.foot(p, k) = xp;
-  R.foot(v, k) = xv;
-  R.foot(acc, k) = xa;
 }
 
 // Foot_trajectory_solve_mod2 (PRMPCClass.cpp:1756-2195), _stopwalking = false
@@ -315,35 +316,82 @@ __device__ void foot_traj_mod2(const Robot &R, int j_indexx, const double nrt[9]
   }
   t_end = (int)round((R.D(F_TX + NS - 1) - 2 * TSTEP) / DT_FAST);  // :1780
   R.D(F_TXTOT) = R.D(F_TX + NS - 1);
-  IndexScan scan;  // goals j*dt, (j+1)*dt, (j+1)*dt, ... never decrease
+  // The four passes below are restated with their memory traffic regrouped
+  // (same arithmetic, same order of operations):
+  //  * _footxyz_real(1, 0) = -stepwidth is written at the head of every pass
+  //    (:1814) -- written once here, before anything reads it;
+  //  * the schedule of all passes first (Indexfind only reads _tx, which no
+  //    pass writes), then every data-dependent load of all passes in one
+  //    batch (_tx/_td/_ts/_lift_height_ref at bjx1-1, _footxyz_real at bjxx
+  //    and bjxx-2): a pass that swings has j_index <= _t_end_footstep, and
+  //    the lift zeroing of :1801-1807 only runs in passes with j_index >
+  //    _t_end_footstep, which come after it, so the lift it reads is the
+  //    stored one, or 0 from :1809-1811 for steps 24..26;
+  //  * the foot positions at k - 1 and _ry_left_right carried in registers
+  //    from pass to pass instead of stored and re-read.
+  R.fxyz(1, 0) = -STEPWIDTH0;  // :1814
+  int xx[NH], x1[NH];
+  {
+    IndexScan scan;  // goals j*dt, (j+1)*dt, (j+1)*dt, ... never decrease
+#pragma unroll
+    for (int kk = 1; kk <= NH; ++kk) {
+      const int j_index = j_indexx + kk - 1;
+      if (j_index <= t_end) {  // :1790-1799
+        bjxx = scan(R, j_index * DT_FAST) + 1;
+        bjx1 = scan(R, (j_index + 1) * DT_FAST) + 1;
+      }
+      xx[kk - 1] = sched_xx[kk - 1] = bjxx;
+      x1[kk - 1] = sched_x1[kk - 1] = bjx1;
+    }
+  }
+  double txb[NH], tdb[NH], tsb[NH], lfb[NH], fx[NH][3], fm[NH][3];
 #pragma unroll
   for (int kk = 1; kk <= NH; ++kk) {
-    const int j_index = j_indexx + kk - 1, k = kk;
-    if (j_index <= t_end) {  // :1790-1799
-      bjxx = scan(R, j_index * DT_FAST) + 1;
-      bjx1 = scan(R, (j_index + 1) * DT_FAST) + 1;
-    }
-    sched_xx[kk - 1] = bjxx;
-    sched_x1[kk - 1] = bjx1;
-    if (j_index > t_end)  // :1801-1807
-      for (int i_t = bjx1 + 1; i_t < NS; i_t++) R.D(F_LIFT + i_t) = 0;
-    for (int i_t = 24; i_t < NS; i_t++) R.D(F_LIFT + i_t) = 0;  // :1809-1811
-    R.fxyz(1, 0) = -STEPWIDTH0;                                 // :1814
-    if ((bjx1 >= 2) && (j_index <= t_end)) {
-      const int b1 = bjx1, bx = bjxx;
+    const int q = kk - 1, j_index = j_indexx + q;
+    if ((x1[q] >= 2) && (j_index <= t_end)) {
+      const int b1 = x1[q], bx = xx[q];
       const int bm = bx >= 2 ? bx - 2 : 0;  // reference UB below 0 (oracle/rt_tick.c)
-      const int sx = (b1 % 2 == 0) ? LX : RX;  // support leg holds
-      const int wx = (b1 % 2 == 0) ? RX : LX;  // swing leg
+      txb[q] = R.D(F_TX + b1 - 1);
+      tdb[q] = R.D(F_TD + b1 - 1);
+      tsb[q] = R.D(F_TS + b1 - 1);
+      lfb[q] = (b1 - 1 >= 24) ? 0.0 : R.D(F_LIFT + b1 - 1);
       for (int ax = 0; ax < 3; ++ax) {
-        const double h = R.foot(sx + ax, k - 1);
+        fx[q][ax] = R.fxyz(ax, bx);
+        fm[q][ax] = R.fxyz(ax, bm);
+      }
+    } else {
+      txb[q] = tdb[q] = tsb[q] = lfb[q] = 0.0;
+      for (int ax = 0; ax < 3; ++ax) fx[q][ax] = fm[q][ax] = 0.0;
+    }
+  }
+  // foot positions at k - 1: right x, y, z then left x, y, z
+  double pos[6];
+  for (int ax = 0; ax < 3; ++ax) {
+    pos[ax] = R.foot(RX + ax, 0);
+    pos[3 + ax] = R.foot(LX + ax, 0);
+  }
+  double rylr = R.D(F_RYLR);
+#pragma unroll
+  for (int kk = 1; kk <= NH; ++kk) {
+    const int q = kk - 1, j_index = j_indexx + q, k = kk;
+    const int b1 = x1[q];
+    if (j_index > t_end)  // :1801-1807
+      for (int i_t = b1 + 1; i_t < NS; i_t++) R.D(F_LIFT + i_t) = 0;
+    for (int i_t = 24; i_t < NS; i_t++) R.D(F_LIFT + i_t) = 0;  // :1809-1811
+    if ((b1 >= 2) && (j_index <= t_end)) {
+      const bool even = (b1 % 2 == 0);
+      const int sx = even ? LX : RX;  // support leg holds
+      const int wx = even ? RX : LX;  // swing leg
+      const int sp = even ? 3 : 0, wp = even ? 0 : 3;  // their slots in pos
+      for (int ax = 0; ax < 3; ++ax) {
+        const double h = pos[sp + ax];
         R.foot(sx + ax, k) = h;
         R.foot(sx + ax, k + 1) = h;
       }
-      const double rt = round(R.D(F_TX + b1 - 1) / DT_FAST);
-      const double tdb = R.D(F_TD + b1 - 1), tsb = R.D(F_TS + b1 - 1);
-      if ((j_index + 1 - rt) * DT_FAST < tdb) {  // double support
+      const double rt = round(txb[q] / DT_FAST);
+      if ((j_index + 1 - rt) * DT_FAST < tdb[q]) {  // double support
         for (int ax = 0; ax < 3; ++ax) {
-          const double h = R.foot(wx + ax, k - 1);
+          const double h = pos[wp + ax];
           R.foot(wx + ax, k) = h;
           R.foot(wx + ax, k + 1) = h;
         }
@@ -351,13 +399,14 @@ __device__ void foot_traj_mod2(const Robot &R, int j_indexx, const double nrt[9]
         const double t_des = (j_index + 1 - rt + 1) * DT_FAST;
         double tp[3];
         tp[0] = t_des - DT_FAST;
-        tp[1] = (tdb + tsb) / 2 + 0.0001;
-        tp[2] = tsb - (2 * DT_FAST + 0.001);
-        if (fabs(t_des - tsb) <= (DT_FAST)) {
+        tp[1] = (tdb[q] + tsb[q]) / 2 + 0.0001;
+        tp[2] = tsb[q] - (2 * DT_FAST + 0.001);
+        if (fabs(t_des - tsb[q]) <= (DT_FAST)) {
           for (int ax = 0; ax < 3; ++ax) {
-            const double e = R.fxyz(ax, bx);
+            const double e = fx[q][ax];
             R.foot(wx + ax, k) = e;
             R.foot(wx + ax, k + 1) = e;
+            pos[wp + ax] = e;
           }
         } else {
           const double A[16] = {cube(tp[0]), sq(tp[0]), (tp[0]), 1,
@@ -366,30 +415,41 @@ __device__ void foot_traj_mod2(const Robot &R, int j_indexx, const double nrt[9]
                                 3 * sq(tp[2]), 2 * (tp[2]), 1.0, 0};
           double Ai[16];
           inv4(A, Ai);  // solve_AAA_inv2 (:2225-2237)
-          swing_axis(R, Ai, t_des, wx + 0, wx + 3, wx + 6, k,
-                     (R.fxyz(0, bm) + R.fxyz(0, bx)) / 2, R.fxyz(0, bx));
-          if ((j_index + 1 - rt) * DT_FAST < tdb + DT_FAST)
-            R.D(F_RYLR) = (R.fxyz(1, bx) + R.fxyz(1, bm)) / 2;
-          swing_axis(R, Ai, t_des, wx + 1, wx + 4, wx + 7, k, R.D(F_RYLR), R.fxyz(1, bx));
-          const double z0 = R.fxyz(2, bm), z1 = R.fxyz(2, bx);
+          if ((j_index + 1 - rt) * DT_FAST < tdb[q] + DT_FAST)
+            rylr = (fx[q][1] + fm[q][1]) / 2;
+          const double z0 = fm[q][2], z1 = fx[q][2];
           const double zmax = (z0 < z1) ? z1 : z0;  // std::max
-          swing_axis(R, Ai, t_des, wx + 2, wx + 5, wx + 8, k, zmax + R.D(F_LIFT + b1 - 1), z1);
-          for (int ax = 0; ax < 3; ++ax)
-            R.foot(wx + ax, k + 1) = R.foot(wx + ax, k) + DT_FAST * R.foot(wx + 3 + ax, k);
+          const double mid[3] = {(fm[q][0] + fx[q][0]) / 2, rylr, zmax + lfb[q]};
+          for (int ax = 0; ax < 3; ++ax) {
+            double xp, xv, xa;
+            swing_axis(Ai, t_des, pos[wp + ax], mid[ax], fx[q][ax], xp, xv, xa);
+            R.foot(wx + ax, k) = xp;
+            R.foot(wx + 3 + ax, k) = xv;
+            R.foot(wx + 6 + ax, k) = xa;
+            R.foot(wx + ax, k + 1) = xp + DT_FAST * xv;
+            pos[wp + ax] = xp;
+          }
         }
       }
     } else {
       if (j_index > t_end) {  // :2152-2160
         for (int ax = 0; ax < 3; ++ax) {
-          R.foot(RX + ax, k) = R.foot(RX + ax, k - 1);
-          R.foot(LX + ax, k) = R.foot(LX + ax, k - 1);
+          R.foot(RX + ax, k) = pos[ax];
+          R.foot(LX + ax, k) = pos[3 + ax];
         }
-      } else {  // :2163-2166
+      } else {  // :2163-2166; the other axes keep their stored values
         R.foot(RY, k) = -STEPWIDTH0;
         R.foot(LY, k) = STEPWIDTH0;
+        pos[1] = -STEPWIDTH0;
+        pos[4] = STEPWIDTH0;
+        pos[0] = R.foot(RX, k);
+        pos[2] = R.foot(RZ, k);
+        pos[3] = R.foot(LX, k);
+        pos[5] = R.foot(LZ, k);
       }
     }
   }
+  R.D(F_RYLR) = rylr;
   for (int j = 0; j < 5; j++) {  // :2170-2178
     R.D(F_FOORPR + 0 + 6 * j) = R.foot(RX, j + 1);
     R.D(F_FOORPR + 1 + 6 * j) = R.foot(RY, j + 1);
