@@ -227,64 +227,74 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
     }
     double pth[BNH];
     for (int jx = 0; jx < BNH; jx++) pth[jx] = K.j_ini / (K.mass * (R3(comacc_ref, 2, jx) + K.g));
-    if (li == 0) {
-      for (int t = 0; t < BNT * BNT; ++t) P.gi.R[t] = 0.0;
-      for (int c = 0; c < BNH; ++c)
-        for (int r = 0; r < BNH; ++r) {  // :511-515
-          const double I = (r == c) ? 1.0 : 0.0;
-          double pp = pth[r] * pth[c];
-          if (r != c) pp = 0.0;
-          const double wx = K.Rthetax / 2 * I + K.alphathetax / 2 * K.pvu_2[c * BNH + r] +
-                            K.beltathetax / 2 * K.ppu_2[c * BNH + r] + K.gama_zmpy / 2 * pp;
-          const double wy = K.Rthetay / 2 * I + K.alphathetay / 2 * K.pvu_2[c * BNH + r] +
-                            K.beltathetay / 2 * K.ppu_2[c * BNH + r] + K.gama_zmpx / 2 * pp;
-          P.gi.R[c * BNT + r] = 2 * wx;
-          P.gi.R[(c + BNH) * BNT + (r + BNH)] = 2 * wy;
-        }
-      double det_px[BNH], det_py[BNH];
+    // QP data (:505-535), one entry set per lane of the 16-lane group (each
+    // entry computed exactly as the serial loops of the reference do)
+    {
+      const int r = li & 3, c = li >> 2;  // G: lane (r, c) of the two 4x4 blocks
+      const double I = (r == c) ? 1.0 : 0.0;  // :511-515
+      double pp = pth[r] * pth[c];
+      if (r != c) pp = 0.0;
+      const double wx = K.Rthetax / 2 * I + K.alphathetax / 2 * K.pvu_2[c * BNH + r] +
+                        K.beltathetax / 2 * K.ppu_2[c * BNH + r] + K.gama_zmpy / 2 * pp;
+      const double wy = K.Rthetay / 2 * I + K.alphathetay / 2 * K.pvu_2[c * BNH + r] +
+                        K.beltathetay / 2 * K.ppu_2[c * BNH + r] + K.gama_zmpx / 2 * pp;
+      P.gi.R[c * BNT + r] = 2 * wx;
+      P.gi.R[(c + BNH) * BNT + (r + BNH)] = 2 * wy;
+      P.gi.R[c * BNT + (r + BNH)] = 0.0;
+      P.gi.R[(c + BNH) * BNT + r] = 0.0;
+    }
+    if (li < BNT) {  // q_goal row li (:523-526): x rows 0..3, y rows 4..7
+      const int r = li & 3;
+      const bool ya = li >= BNH;
+      const double *tk = ya ? thetayk : thetaxk;
+      double v = 0, pq = 0, ref = 0;
       for (int k = 0; k < BNH; ++k) {
-        det_px[k] = R2(zmp_ref, 0, k) - copx[k];
-        det_py[k] = R2(zmp_ref, 1, k) - copy[k];
+        const double pvs_t = K.pvs[k] * tk[0] + K.pvs[BNH + k] * tk[1];
+        const double pps_t = K.pps[k] * tk[0] + K.pps[BNH + k] * tk[1];
+        v += K.pvu[r * BNH + k] * pvs_t;
+        pq += K.ppu[r * BNH + k] * pps_t;
+        ref += K.ppu[r * BNH + k] * R2(angle_ref, ya ? 1 : 0, k);
       }
-      for (int r = 0; r < BNH; ++r) {  // q_goal, :523-526
-        double pvs_tx, pps_tx, pvs_ty, pps_ty;
-        double vx = 0, px = 0, vy = 0, py = 0, refx = 0, refy = 0;
-        for (int k = 0; k < BNH; ++k) {
-          pvs_tx = K.pvs[k] * thetaxk[0] + K.pvs[BNH + k] * thetaxk[1];
-          pps_tx = K.pps[k] * thetaxk[0] + K.pps[BNH + k] * thetaxk[1];
-          pvs_ty = K.pvs[k] * thetayk[0] + K.pvs[BNH + k] * thetayk[1];
-          pps_ty = K.pps[k] * thetayk[0] + K.pps[BNH + k] * thetayk[1];
-          vx += K.pvu[r * BNH + k] * pvs_tx;
-          px += K.ppu[r * BNH + k] * pps_tx;
-          vy += K.pvu[r * BNH + k] * pvs_ty;
-          py += K.ppu[r * BNH + k] * pps_ty;
-          refx += K.ppu[r * BNH + k] * R2(angle_ref, 0, k);
-          refy += K.ppu[r * BNH + k] * R2(angle_ref, 1, k);
-        }
-        P.g0[r] = K.alphathetax * vx + K.beltathetax * px - K.beltathetax * refx +
-                  K.gama_zmpy * pth[r] * det_py[r];
-        P.g0[BNH + r] = K.alphathetay * vy + K.beltathetay * py - K.beltathetay * refy +
-                        K.gama_zmpx * (-pth[r]) * det_px[r];
+      if (!ya) {
+        const double det_py = R2(zmp_ref, 1, r) - copy[r];
+        P.g0[r] = K.alphathetax * v + K.beltathetax * pq - K.beltathetax * ref +
+                  K.gama_zmpy * pth[r] * det_py;
+      } else {
+        const double det_px = R2(zmp_ref, 0, r) - copx[r];
+        P.g0[BNH + r] = K.alphathetay * v + K.beltathetay * pq - K.beltathetay * ref +
+                        K.gama_zmpx * (-pth[r]) * det_px;
       }
-      for (int t = 0; t < BNI; ++t) P.ci0[t] = 0.0;
-      for (int row = 0; row < BNH; ++row) {
-        const double ppsx = K.pps[row] * thetaxk[0] + K.pps[BNH + row] * thetaxk[1];
-        const double ppsy = K.pps[row] * thetayk[0] + K.pps[BNH + row] * thetayk[1];
-        P.ci0[0 * BNH + row] = K.thetax_max - ppsx;
-        P.ci0[1 * BNH + row] = -K.thetax_min + ppsx;
-        P.ci0[2 * BNH + row] = K.thetay_max - ppsy;
-        P.ci0[3 * BNH + row] = -K.thetay_min + ppsy;
-        P.ci0[4 * BNH + row] = K.torque_max;
-        P.ci0[5 * BNH + row] = -K.torque_min;
-        P.ci0[6 * BNH + row] = K.torque_max;
-        P.ci0[7 * BNH + row] = -K.torque_min;
+    }
+    {  // ci0 (:527-535): lane (row, block pair); entries 32..47 stay 0
+      const int row = li & 3, bp = li >> 2;
+      const double ppsx = K.pps[row] * thetaxk[0] + K.pps[BNH + row] * thetaxk[1];
+      const double ppsy = K.pps[row] * thetayk[0] + K.pps[BNH + row] * thetayk[1];
+      double e0, e1;
+      if (bp == 0) {
+        e0 = K.thetax_max - ppsx;
+        e1 = -K.thetax_min + ppsx;
+      } else if (bp == 1) {
+        e0 = K.thetay_max - ppsy;
+        e1 = -K.thetay_min + ppsy;
+      } else {
+        e0 = K.torque_max;
+        e1 = -K.torque_min;
       }
+      P.ci0[(2 * bp) * BNH + row] = e0;
+      P.ci0[(2 * bp + 1) * BNH + row] = e1;
+      P.ci0[8 * BNH + li] = 0.0;
     }
     GI_SYNC();
     double f;
     int it;
+#ifndef QLOCO_ABLATE_BODY_GI
     gi_solve_group(P.gi, li, BNT, 0, BNI, P.gi.R, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
                    status, it);
+#else  // timing experiments only (tools/variant_lib.py): setup + outputs without the solve
+    if (li < BNT) P.x[li] = P.g0[li] * 1e-9;
+    f = 0.0;
+    it = 0;
+#endif
     GI_SYNC();
     if (li == 0) {
       bool ok = true;

@@ -144,6 +144,9 @@ def main():
     if args.support:
         return bench_support(args)
     import torch
+    if os.environ.get("QLOCO_LIB"):  # experimental variant (tools/variant_lib.py)
+        from quadrupedal_loco_amd import _lib
+        _lib.LIB_PATH = os.environ["QLOCO_LIB"]
     from quadrupedal_loco_amd.rt import RtNodeBatch, synth_messages
     B, M = args.robots, args.sets
     dev = torch.device("cuda:0")
