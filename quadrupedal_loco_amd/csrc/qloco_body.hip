@@ -162,12 +162,6 @@ __device__ __forceinline__ int indexfind(const BodyConsts &k, double goal) {
   while (j < BSTEPS && goal >= k.tx[j]) j++;
   return j - 1;
 }
-// ... on a per-robot schedule (strided)
-__device__ __forceinline__ int indexfind(const double *tx, int64_t stride, double goal) {
-  int j = 0;
-  while (j < BSTEPS && goal >= tx[j * stride]) j++;
-  return j - 1;
-}
 
 #define R2(m, r, c) ((m)[(c)*2 + (r)])
 #define R3(m, r, c) ((m)[(c)*3 + (r)])
@@ -200,9 +194,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
   if (active) {
     const double t_f0 = (i + 1) * K.dt_mpc, t_f3 = (i + BNH) * K.dt_mpc;  // :406
     if (a.tx) {
+      // the robot's _tx: lane li of the group holds entries li and li + 16,
+      // loaded together; Indexfind's stopping index (the first j with
+      // goal < _tx(j), 27 if none) is the lowest set bit of a ballot --
+      // the same answer as the scan for any _tx, one load round trip
       const double *txr = a.tx + (a.tx_tile > 0 ? (inst >> 6) * a.tx_tile + (inst & 63) : inst);
-      bjx1 = indexfind(txr, a.tx_stride, t_f0) + 1;
-      bjx2 = indexfind(txr, a.tx_stride, t_f3) + 1;
+      const bool v1 = li + 16 < BSTEPS;
+      const double t0 = txr[li * a.tx_stride];
+      const double t1 = v1 ? txr[(li + 16) * a.tx_stride] : 0.0;
+      auto first_below = [&](double goal) {
+        const uint64_t m0 = (__ballot(goal < t0) >> (16 * grp)) & 0xFFFFull;
+        const uint64_t m1 = (__ballot(v1 && goal < t1) >> (16 * grp)) & 0xFFFFull;
+        return m0 ? __builtin_ctzll(m0) : (m1 ? 16 + __builtin_ctzll(m1) : BSTEPS);
+      };
+      bjx1 = first_below(t_f0);  // Indexfind + 1 = stopping index
+      bjx2 = first_below(t_f3);
     } else {
       bjx1 = indexfind(K, t_f0) + 1;
       bjx2 = indexfind(K, t_f3) + 1;

@@ -333,6 +333,14 @@ __device__ void foot_traj_mod2(const Robot &R, int j_indexx, const double nrt[9]
   int xx[NH], x1[NH];
   {
     IndexScan scan;  // goals j*dt, (j+1)*dt, (j+1)*dt, ... never decrease
+    // and across ticks: resume near last tick's answer when goal >= _tx(j0-1)
+    // (then every earlier entry passes too, _tx being non-decreasing), so
+    // the scan costs O(1) loads however far the robot has walked
+    {
+      const int j0 = bjxx - 1;
+      if (j0 >= 1 && j0 <= NS && j_indexx <= t_end && j_indexx * DT_FAST >= R.D(F_TX + j0 - 1))
+        scan.j = j0;
+    }
 #pragma unroll
     for (int kk = 1; kk <= NH; ++kk) {
       const int j_index = j_indexx + kk - 1;
