@@ -657,13 +657,19 @@ __global__ __launch_bounds__(PRE_T) void rt_pre_kernel(const RtArgs a) {
         const int mpc = R.I(I_MPC) + 1;
         R.I(I_MPC) = mpc;
         int t_end = R.I(I_TEND);
+#ifndef QLOCO_ABLATE_RT_INTERP  // timing experiments only (tools/gpu_rt_ablate.sh)
         interpolation(a, R, g, flag, t_int, t_end);
+#endif
         if (mpc * DT_FAST > 1.0) {  // _height_offset_timex = 1 (:537-545)
           const int foot_i = (int)(mpc - (int)1.0 / DT_FAST);
           int bjx1 = (int)body[26], bjxx = R.I(I_BJXX);
           int sxx[NH], sx1[NH];
+#ifndef QLOCO_ABLATE_RT_FOOT  // timing experiments only
           foot_traj_mod2(R, foot_i, nrt, bjx1, bjxx, t_end, sxx, sx1);
+#ifndef QLOCO_ABLATE_RT_ROT
           foot_rotation(R, foot_i, bjx1, bjxx, t_end, sxx, sx1);
+#endif
+#endif
           body[26] = bjx1;
           R.I(I_BJXX) = bjxx;
           R.I(I_TEND) = t_end;
@@ -680,8 +686,10 @@ __global__ __launch_bounds__(PRE_T) void rt_pre_kernel(const RtArgs a) {
   }
   // the reference record of every robot (read by body_mpc_kernel only where
   // run = 1), written row-coalesced
+#ifndef QLOCO_ABLATE_RT_REF  // timing experiments only
   stage_rows<PRE_T>(stage, tid, nb, r0, live, RF_USED, reinterpret_cast<double *>(a.ws + L.ref),
                     RF_LD, 0, [&](int k) { return ref_slot(R, ctrl, k); });
+#endif
 }
 
 // /rtMPC/traj slot k in [36, 100) of robot R: low_mpc_gait_inte(k - 36)
