@@ -695,8 +695,8 @@ __global__ __launch_bounds__(PRE_T) void rt_pre_kernel(const RtArgs a) {
 // /rtMPC/traj slot k in [36, 100) of robot R: low_mpc_gait_inte(k - 36)
 // (gait_fast.cpp:633-714), the untouched [87, 98), (int)_tx_total/0.001 and
 // the loop count (:727-729)
-__device__ __forceinline__ double traj_slot(const Robot &R, const double *body,
-                                            const double *g, int k) {
+__device__ __forceinline__ double traj_slot(const Robot &R, const double *body, double g27,
+                                            int k) {
   const int u = k - 36;
   if (u < 3) return R.D(F_RPY + u);                       // rpy_mpc_body
   if (u < 5) return R.D(F_BTHX + u - 3);                  // body_thetax(0..1)
@@ -706,7 +706,7 @@ __device__ __forceinline__ double traj_slot(const Robot &R, const double *body,
   if (u < 14) return R.D(F_ZINT + u - 12);                // zmp_inter(0..1)
   if (u == 14) return R.D(F_ZMP + 8);                     // zmpxyz_ref(2)
   if (u < 27) return 0.0;                                 // F_L, F_R, M_L, M_R
-  if (u == 27) return g[27];                              // bjx1 of /MPC/Gait
+  if (u == 27) return g27;                                // bjx1 of /MPC/Gait[27]
   if (u < 31) return R.D(F_FTHETA + 3 + (u - 28));        // left foot rpy
   if (u < 34) return R.D(F_FTHETA + (u - 31));            // right foot rpy
   if (u < 36) return R.D(F_DINT + u - 34);                // dcm_inter(0..1)
@@ -717,36 +717,72 @@ __device__ __forceinline__ double traj_slot(const Robot &R, const double *body,
   return R.I(I_LOOP);                                     // count_in_rt_loop
 }
 
-constexpr int POST_T = 256;  // robots per block
+constexpr int POST_R = 64;             // robots per block (one state tile)
+constexpr int POST_P = 4;              // waves per block: slot quarters
+constexpr int POST_T = POST_R * POST_P;
+constexpr int POST_LD = 65;            // LDS row stride (doubles), odd
 
-// Each lane computes its robot's slots; the block then writes the rows of its
-// robots cooperatively (a per-lane row store touches 64 lines per
-// instruction, the staged store 2-3).
+// Wave p of the block computes its quarter of the slots for the block's 64
+// robots (one state tile: every field read is one coalesced 512-byte row),
+// into an LDS copy of the rows; the block then writes whole rows (a wave
+// stores 512 contiguous bytes).  Four waves per 64 robots keep four times
+// the memory requests in flight of one-robot-per-lane-for-all-slots.
+template <int P>
+__device__ __forceinline__ void post_part(const Robot &R, const double *body, double g27,
+                                          double *st, int rr, bool live) {
+  if (!live) return;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) st[rr * POST_LD + 16 * P + j] = traj_slot(R, body, g27, 36 + 16 * P + j);
+}
+
 __global__ __launch_bounds__(POST_T) void rt_post_kernel(const RtArgs a) {
-  __shared__ double stage[POST_T * STG_LD];
-  const int tid = threadIdx.x;
-  const int64_t B = a.B, r0 = (int64_t)blockIdx.x * POST_T;
-  const int nb = (int)((B - r0) < POST_T ? (B - r0) : POST_T);
-  const int64_t r = r0 + tid;
-  const bool live = tid < nb;
+  __shared__ double stage[POST_R * POST_LD];
+  const int tid = threadIdx.x, rr = tid & (POST_R - 1), part = tid >> 6;
+  const int64_t B = a.B, r0 = (int64_t)blockIdx.x * POST_R;
+  const int nb = (int)((B - r0) < POST_R ? (B - r0) : POST_R);
+  const int64_t r = r0 + rr;
+  const bool live = rr < nb;
   const Ws L = layout(B);
   Robot R(a.ws, L, r);
   const double *body = reinterpret_cast<const double *>(a.ws + L.body) + r * QLOCO_BODY_STATE_LEN;
-  const double *g = a.gait + r * QLOCO_GAIT_MSG_LEN;
   // [0, 36): the /MPC/Gait rows copied through (:716-719)
   for (int idx = tid; idx < nb * 36; idx += POST_T) {
-    const int rr = idx / 36, k = idx - rr * 36;
-    a.traj[(r0 + rr) * QLOCO_TRAJ_MSG_LEN + k] = a.gait[(r0 + rr) * QLOCO_GAIT_MSG_LEN + k];
+    const int q = idx / 36, k = idx - q * 36;
+    a.traj[(r0 + q) * QLOCO_TRAJ_MSG_LEN + k] = a.gait[(r0 + q) * QLOCO_GAIT_MSG_LEN + k];
   }
-  stage_rows<POST_T>(stage, tid, nb, r0, live, 64, a.traj, QLOCO_TRAJ_MSG_LEN, 36,
-            [&](int k) { return traj_slot(R, body, g, 36 + k); });
-  // /rt2nrt/state (last published state_to_MPC)
-  stage_rows<POST_T>(stage, tid, nb, r0, live, 25, a.nrt, QLOCO_NRT_MSG_LEN, 0,
-            [&](int k) { return R.D(F_NRT + k); });
-  if (a.gen)  // debug dump: foorpr_gen | foortheta_gen (contiguous fields)
-    stage_rows<POST_T>(stage, tid, nb, r0, live, 60, a.gen, 60, 0,
-              [&](int k) { return R.D(F_FOORPR + k); });
-  if (a.sched && live) {
+  // [36, 100): low_mpc_gait_inte etc., a quarter per wave
+  const double g27 = live ? a.gait[r * QLOCO_GAIT_MSG_LEN + 27] : 0.0;
+  switch (part) {  // wave-uniform
+    case 0: post_part<0>(R, body, g27, stage, rr, live); break;
+    case 1: post_part<1>(R, body, g27, stage, rr, live); break;
+    case 2: post_part<2>(R, body, g27, stage, rr, live); break;
+    default: post_part<3>(R, body, g27, stage, rr, live); break;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < nb * 64; idx += POST_T) {
+    const int q = idx >> 6, j = idx & 63;
+    a.traj[(r0 + q) * QLOCO_TRAJ_MSG_LEN + 36 + j] = stage[q * POST_LD + j];
+  }
+  __syncthreads();
+  // /rt2nrt/state (last published state_to_MPC): slots k = part + 4i
+  if (live)
+    for (int k = part; k < 25; k += POST_P) stage[rr * POST_LD + k] = R.D(F_NRT + k);
+  __syncthreads();
+  for (int idx = tid; idx < nb * 25; idx += POST_T) {
+    const int q = idx / 25, j = idx - q * 25;
+    a.nrt[(r0 + q) * QLOCO_NRT_MSG_LEN + j] = stage[q * POST_LD + j];
+  }
+  if (a.gen) {  // debug dump: foorpr_gen | foortheta_gen (contiguous fields)
+    __syncthreads();
+    if (live)
+      for (int k = part; k < 60; k += POST_P) stage[rr * POST_LD + k] = R.D(F_FOORPR + k);
+    __syncthreads();
+    for (int idx = tid; idx < nb * 60; idx += POST_T) {
+      const int q = idx / 60, j = idx - q * 60;
+      a.gen[(r0 + q) * 60 + j] = stage[q * POST_LD + j];
+    }
+  }
+  if (a.sched && live && part == 0) {
     const int32_t run = *(reinterpret_cast<const int32_t *>(a.ws + L.run) + r);
     const int32_t bst = *(reinterpret_cast<const int32_t *>(a.ws + L.st) + r);
     const double *ctrl = a.ctrl + r * QLOCO_CTRL_MSG_LEN;
@@ -942,7 +978,7 @@ extern "C" int qloco_rt_tick(int64_t batch, void *workspace, const double *gait_
       (const double *)(w + L.d) + rt::F_TX * rt::TL, rt::TL, rt::F_DOUBLES * rt::TL,
       (const int32_t *)(w + L.run), rt::RF_LD, s);
   if (rc != QLOCO_OK) return rc;
-  hipLaunchKernelGGL(rt::rt_post_kernel, dim3((unsigned)((batch + rt::POST_T - 1) / rt::POST_T)),
+  hipLaunchKernelGGL(rt::rt_post_kernel, dim3((unsigned)((batch + rt::POST_R - 1) / rt::POST_R)),
                      dim3(rt::POST_T), 0, s, a);
   QLOCO_HIP_CHECK(hipGetLastError(), "rt_post_kernel launch");
   return QLOCO_OK;
