@@ -91,6 +91,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--overlap", action="store_true",
+                    help="N > 1: run each step's all-gather under the next solve (double-"
+                         "buffered u0); off by default: on one GPU the RCCL kernel sharing "
+                         "the CUs with the solve cost more than it hid (DESIGN.md §7)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="testing: run the N > 1 code path (RCCL group, all-gather) at N = 1")
     args = ap.parse_args()
 
     import torch
@@ -101,7 +107,13 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    json_out = sys.stdout
+    if world > 1 or args.force_dist:
+        # RCCL prints a version banner on stdout when its communicator comes
+        # up: keep stdout for the one JSON line, library output goes to stderr
+        sys.stdout.flush()
+        json_out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
@@ -117,20 +129,46 @@ def main():
     d_ct = torch.from_numpy(ct).to(dev)
     solver = srbd.BatchedConvexMpc(horizon=N)
     legs = srbd.max_stance_legs(ct, N)
-    out = solver.alloc_outputs(B, dev)
     gather = None
-    if world > 1 and not args.no_allgather:
+    multi = world > 1 or args.force_dist
+    overlap = multi and not args.no_allgather and args.overlap
+    if multi and not args.no_allgather:
         from quadrupedal_loco_amd.dist import ForceGather
-        gather = ForceGather(B, device=dev)
+        gather = [ForceGather(B, device=dev) for _ in range(2 if overlap else 1)]
+    # two output sets when the all-gather of step i overlaps the solve of step
+    # i + 1: step i solves into set i % 2, after the gather that last read it
+    outs = [solver.alloc_outputs(B, dev) for _ in range(2 if overlap else 1)]
+    out = outs[0]
     stream = torch.cuda.current_stream(dev)
+    pending = [None, None]
 
-    def step():
-        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, max_legs=legs, stream=stream.cuda_stream)
+    def step(i, ev=None):
+        o = outs[i % len(outs)]
+        if pending[i % 2] is not None:  # the gather that last read this u0 set
+            pending[i % 2].wait()
+            pending[i % 2] = None
+        if ev is not None:
+            ev[0].record(stream)
+        solver.solve(d_x0, d_xr, d_ft, d_ct, out=o, max_legs=legs, stream=stream.cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
         if gather is not None:
-            gather(out.u0)
+            if overlap:
+                _, pending[i % 2] = gather[i % 2](o.u0, async_op=True)
+            else:
+                gather[0](o.u0)
+        if ev is not None:
+            ev[2].record(stream)
 
-    for _ in range(args.warmup):
-        step()
+    def drain():
+        for k in range(2):
+            if pending[k] is not None:
+                pending[k].wait()
+                pending[k] = None
+
+    for i in range(args.warmup):
+        step(i)
+    drain()
     torch.cuda.synchronize(dev)
 
     K = args.steps
@@ -142,12 +180,8 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(K):
-        ev_s[i].record(stream)
-        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, max_legs=legs, stream=stream.cuda_stream)
-        ev_k[i].record(stream)
-        if gather is not None:
-            gather(out.u0)
-        ev_e[i].record(stream)
+        step(i, (ev_s[i], ev_k[i], ev_e[i]))
+    drain()
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -191,7 +225,8 @@ def main():
                         % (args.gait, N, B, _config_tag(N, args.gait, B)),
             "horizon": N, "batch_per_gpu": B, "gait": args.gait,
             "solver": "OSQP-algorithm ADMM, default settings (eps 1e-3, adaptive rho)",
-            "parallelism": "dp%d (instance shards, RCCL all-gather of u0)" % world,
+            "parallelism": "dp%d (instance shards, RCCL all-gather of u0%s)" % (
+                world, ", overlapped with the next solve" if overlap else ""),
         },
         "p99_batch_us": round(float(np.percentile(step_ms, 99)) * 1e3, 2),
         "p50_batch_us": round(float(np.percentile(step_ms, 50)) * 1e3, 2),
@@ -223,7 +258,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(N, args.gait, args.cpu_seconds, args.cpu_threads)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=json_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

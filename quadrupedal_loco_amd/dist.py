@@ -42,11 +42,18 @@ class ForceGather:
         if not self._flat:
             self._views = list(self.out.split(per_rank))
 
-    def __call__(self, u0):
+    def __call__(self, u0, async_op=False):
+        """Gather u0 of every rank into self.out.  async_op=True returns
+        (out, work): the collective runs on the backend's stream (after the
+        work already queued on the current one) and work.wait() makes the
+        current stream wait for it -- so a caller can solve the next batch
+        into another u0 buffer while this one is in flight."""
         if u0.shape[0] != self.per_rank:
             raise ValueError("u0 has %d rows, expected %d" % (u0.shape[0], self.per_rank))
         if self._flat:
-            tdist.all_gather_into_tensor(self.out, u0.contiguous(), group=self.group)
+            work = tdist.all_gather_into_tensor(self.out, u0.contiguous(), group=self.group,
+                                                async_op=async_op)
         else:  # gloo has no flat all-gather
-            tdist.all_gather(self._views, u0.contiguous(), group=self.group)
-        return self.out
+            work = tdist.all_gather(self._views, u0.contiguous(), group=self.group,
+                                    async_op=async_op)
+        return (self.out, work) if async_op else self.out

@@ -54,10 +54,19 @@ def _worker(rank, world, port, gait, outdir):
     u0 = torch.from_numpy(_oracle_u0(first, count, gait))
     gather = qdist.ForceGather(PER_RANK)
     out = gather(u0)
+    # bench.py's overlapped form: two gathers in flight on two u0 sets
+    ga, gb = qdist.ForceGather(PER_RANK), qdist.ForceGather(PER_RANK)
+    u0b = u0 * 2
+    oa, wa = ga(u0, async_op=True)
+    ob, wb = gb(u0b, async_op=True)
+    wb.wait()
+    wa.wait()
     t = torch.tensor([float(rank + 1)])
     tdist.all_reduce(t, op=tdist.ReduceOp.MAX)   # the bench's max-over-ranks timing reduction
     if rank == 0:
         np.save(os.path.join(outdir, "gathered.npy"), out.numpy())
+        np.save(os.path.join(outdir, "gathered_a.npy"), oa.numpy())
+        np.save(os.path.join(outdir, "gathered_b.npy"), ob.numpy())
         np.save(os.path.join(outdir, "tmax.npy"), t.numpy())
     tdist.barrier()
     tdist.destroy_process_group()
@@ -72,6 +81,8 @@ def test_gloo_world2_shard_and_allgather(tmp_path, gait):
     ref = _oracle_u0(0, world * PER_RANK, gait)
     assert got.shape == (world * PER_RANK, 12)
     assert np.array_equal(got, ref)
+    assert np.array_equal(np.load(tmp_path / "gathered_a.npy"), ref)
+    assert np.array_equal(np.load(tmp_path / "gathered_b.npy"), ref * 2)
     assert np.load(tmp_path / "tmax.npy")[0] == world
 
 
