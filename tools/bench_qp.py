@@ -87,6 +87,9 @@ def main():
     if args.servo:
         return servo_main(args)
     import torch
+    if os.environ.get("QLOCO_LIB"):  # experimental variant (tools/variant_lib.py)
+        from quadrupedal_loco_amd import _lib
+        _lib.LIB_PATH = os.environ["QLOCO_LIB"]
     from cases import force_inputs
     from quadrupedal_loco_amd import qp
     B = args.robots
