@@ -166,8 +166,9 @@ __device__ __forceinline__ int indexfind(const BodyConsts &k, double goal) {
 #define R2(m, r, c) ((m)[(c)*2 + (r)])
 #define R3(m, r, c) ((m)[(c)*3 + (r)])
 
-// 2 waves/SIMD: the LDS (19 KB per 4-robot block) admits 8 blocks per CU; the
-// register budget is set to match (160 VGPRs, no spills)
+// The LDS (11.6 KB per 4-robot block) admits 13 blocks per CU; the compiler
+// lands at 156 VGPRs (no spills) for the 2-waves/SIMD floor set here, i.e.
+// 3 waves/SIMD -- both limits agree
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void body_mpc_kernel(const BodyArgs a) {
   __shared__ BodyLds S;
   const BodyConsts &K = c_body_K;
