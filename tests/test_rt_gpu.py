@@ -83,6 +83,15 @@ def test_rt_tick_matches_oracle_every_tick():
     assert h["body"] > 0 and h["swing"] > 0 and h["stop"] > 0
 
 
+def test_rt_tick_ragged_batch():
+    """B = 100: one full 64-robot state tile and a partial one (the rt
+    workspace is tiled, the body kernel packs 4 robots per wave), every tick
+    of the first 400 checked against the oracle"""
+    dev = _dev()
+    h = _run(B=100, T=400, dev=dev, first=1000)
+    assert h["body"] > 0 and h["swing"] > 0
+
+
 def test_rt_tick_large_batch_sampled():
     """B = 32768 robots for 300 ticks; the integers and messages of a
     strided sample of robots checked against the oracle run on those robots
