@@ -600,95 +600,102 @@ __device__ __forceinline__ double ref_slot(const Robot &R, const double *ctrl, i
   return j == 0 ? R.D(F_CACC + 2) : R.D(F_CACC + 8 + 3 * j);
 }
 
-constexpr int PRE_T = 256;   // robots per block
-constexpr int STG_C = 16;    // slots per transpose chunk
-constexpr int STG_LD = 17;   // LDS row stride (doubles): odd, conflict-free column reads
+constexpr int PRE_R = 64;           // robots per block (one state tile)
+constexpr int PRE_T = 2 * PRE_R;    // wave 0: callbacks + interpolation, wave 1: foot generators
+constexpr int STG_C = 16;           // slots per transpose chunk
+constexpr int STG_LD = 17;          // LDS row stride (doubles): odd, conflict-free column reads
 
-// Stage `count` slots of every robot of the block (value(k) for k < count)
-// through LDS and store them to out[(r0 + robot) * ld + off + k], so that
-// consecutive lanes write consecutive doubles of a row (a per-lane row store
-// touches 64 cache lines per instruction, the staged one 2-3).
-template <int T, typename F>
-__device__ __forceinline__ void stage_rows(double *stage, int tid, int nb, int64_t r0, bool live,
-                                           int count, double *out, int ld, int off, F value) {
-#pragma unroll
-  for (int c0 = 0; c0 < count; c0 += STG_C) {
-    const int w = (count - c0) < STG_C ? (count - c0) : STG_C;
-    if (live)
-#pragma unroll
-      for (int j = 0; j < STG_C; ++j)
-        if (j < w) stage[tid * STG_LD + j] = value(c0 + j);
-    __syncthreads();
-    for (int idx = tid; idx < nb * w; idx += T) {
-      const int rr = idx / w, j = idx - rr * w;
-      out[(r0 + rr) * ld + off + c0 + j] = stage[rr * STG_LD + j];
-    }
-    __syncthreads();
-  }
-}
-
+// One tile of 64 robots per block, two waves: the loop counters, the
+// published state and the four cubic interpolations (wave 0) and the foot
+// trajectory / rotation generators (wave 1) read and write disjoint fields,
+// so they run side by side; what both need from the previous tick
+// (count_in_mpc, _t_end_footstep) is read before either writes.  Then both
+// waves write the body-MPC reference records, row-coalesced through LDS.
 __global__ __launch_bounds__(PRE_T) void rt_pre_kernel(const RtArgs a) {
-  __shared__ double stage[PRE_T * STG_LD];
-  const int tid = threadIdx.x;
-  const int64_t B = a.B, r0 = (int64_t)blockIdx.x * PRE_T;
-  const int nb = (int)((B - r0) < PRE_T ? (B - r0) : PRE_T);
-  const int64_t r = r0 + tid;
-  const bool live = tid < nb;
+  __shared__ double stage[PRE_R * STG_LD];
+  const int tid = threadIdx.x, rr = tid & (PRE_R - 1), role = tid >> 6;
+  const int64_t B = a.B, r0 = (int64_t)blockIdx.x * PRE_R;
+  const int nb = (int)((B - r0) < PRE_R ? (B - r0) : PRE_R);
+  const int64_t r = r0 + rr;
+  const bool live = rr < nb;
   const Ws L = layout(B);
   Robot R(a.ws, L, r);
   const double *ctrl = a.ctrl + r * QLOCO_CTRL_MSG_LEN;
-  int do_body = 0;
+  const double *g = a.gait + r * QLOCO_GAIT_MSG_LEN;
+  double *body = reinterpret_cast<double *>(a.ws + L.body) + r * QLOCO_BODY_STATE_LEN;
+  // callbacks (:79-110): the loop body runs when /control2rtmpc/state[0] > 0,
+  // the MPC part when mpc_gait_flag = (int)/MPC/Gait[99] > 0
+  bool pub = false, walk = false;
+  int flag = 0, mpc = 0, t_end = 0;
   if (live) {
-    double *body = reinterpret_cast<double *>(a.ws + L.body) + r * QLOCO_BODY_STATE_LEN;
-    int32_t *bi = reinterpret_cast<int32_t *>(a.ws + L.bi) + r;
-    const double *g = a.gait + r * QLOCO_GAIT_MSG_LEN;
-    // callbacks (:79-110)
-    const int flag = (int)g[99];
-    double nrt[9];
-    for (int k = 0; k < 9; ++k) nrt[k] = g[86 + k];
-    if (ctrl[0] > 0) {
+    flag = (int)g[99];
+    pub = ctrl[0] > 0;
+    walk = pub && flag > 0;
+    if (walk) {
+      mpc = R.I(I_MPC) + 1;
+      t_end = R.I(I_TEND);
+    }
+  }
+  __syncthreads();  // both waves have read the previous tick's counters
+  if (live && role == 0) {
+    if (pub) {
       const int loop = R.I(I_LOOP) + 1;
       R.I(I_LOOP) = loop;
       const int t_int = (int)((uint32_t)R.I(I_TINT) + (uint32_t)(int)floor((double)(loop / 2)));
       R.I(I_TINT) = t_int;
       R.D(F_NRT + 0) = t_int;  // state_to_MPC = state_feedback (:519-527)
       for (int k = 1; k < 25; ++k) R.D(F_NRT + k) = ctrl[k];
-      if (flag > 0) {
-        const int mpc = R.I(I_MPC) + 1;
+      if (walk) {
         R.I(I_MPC) = mpc;
-        int t_end = R.I(I_TEND);
 #ifndef QLOCO_ABLATE_RT_INTERP  // timing experiments only (tools/gpu_rt_ablate.sh)
         interpolation(a, R, g, flag, t_int, t_end);
 #endif
-        if (mpc * DT_FAST > 1.0) {  // _height_offset_timex = 1 (:537-545)
-          const int foot_i = (int)(mpc - (int)1.0 / DT_FAST);
-          int bjx1 = (int)body[26], bjxx = R.I(I_BJXX);
-          int sxx[NH], sx1[NH];
-#ifndef QLOCO_ABLATE_RT_FOOT  // timing experiments only
-          foot_traj_mod2(R, foot_i, nrt, bjx1, bjxx, t_end, sxx, sx1);
-#ifndef QLOCO_ABLATE_RT_ROT
-          foot_rotation(R, foot_i, bjx1, bjxx, t_end, sxx, sx1);
-#endif
-#endif
-          body[26] = bjx1;
-          R.I(I_BJXX) = bjxx;
-          R.I(I_TEND) = t_end;
-        }
         R.D(F_ZMP + 8) = 0.0;  // zmpxyz_ref(2) = _Zsc = {l,r}foot_inter(2) = 0 (:557-566)
-        // body_thetax(0..1) = bodyangle_mpc_ref(:, 0) (:590-591)
-        R.D(F_BTHX + 0) = (R.D(F_FTHETA + 0) + R.D(F_FTHETA + 3)) / 5;
-        R.D(F_BTHX + 1) = (R.D(F_FTHETA + 1) + R.D(F_FTHETA + 4)) / 5;
-        *bi = mpc;
-        do_body = 1;
+        *(reinterpret_cast<int32_t *>(a.ws + L.bi) + r) = mpc;
       }
     }
-    *(reinterpret_cast<int32_t *>(a.ws + L.run) + r) = do_body;
+    *(reinterpret_cast<int32_t *>(a.ws + L.run) + r) = walk ? 1 : 0;
+  }
+  if (live && role == 1 && walk && mpc * DT_FAST > 1.0) {  // _height_offset_timex = 1 (:537-545)
+    double nrt[9];
+    for (int k = 0; k < 9; ++k) nrt[k] = g[86 + k];
+    const int foot_i = (int)(mpc - (int)1.0 / DT_FAST);
+    int bjx1 = (int)body[26], bjxx = R.I(I_BJXX), te = t_end;
+    int sxx[NH], sx1[NH];
+#ifndef QLOCO_ABLATE_RT_FOOT  // timing experiments only
+    foot_traj_mod2(R, foot_i, nrt, bjx1, bjxx, te, sxx, sx1);
+#ifndef QLOCO_ABLATE_RT_ROT
+    foot_rotation(R, foot_i, bjx1, bjxx, te, sxx, sx1);
+#endif
+#endif
+    body[26] = bjx1;
+    R.I(I_BJXX) = bjxx;
+    R.I(I_TEND) = te;
+  }
+  __syncthreads();  // the foot generator's fields are visible to wave 0
+  if (live && role == 0 && walk) {
+    // body_thetax(0..1) = bodyangle_mpc_ref(:, 0) (:590-591)
+    R.D(F_BTHX + 0) = (R.D(F_FTHETA + 0) + R.D(F_FTHETA + 3)) / 5;
+    R.D(F_BTHX + 1) = (R.D(F_FTHETA + 1) + R.D(F_FTHETA + 4)) / 5;
   }
   // the reference record of every robot (read by body_mpc_kernel only where
-  // run = 1), written row-coalesced
+  // run = 1), written row-coalesced; the two waves take alternate slots
 #ifndef QLOCO_ABLATE_RT_REF  // timing experiments only
-  stage_rows<PRE_T>(stage, tid, nb, r0, live, RF_USED, reinterpret_cast<double *>(a.ws + L.ref),
-                    RF_LD, 0, [&](int k) { return ref_slot(R, ctrl, k); });
+  double *ref = reinterpret_cast<double *>(a.ws + L.ref);
+#pragma unroll
+  for (int c0 = 0; c0 < RF_USED; c0 += STG_C) {
+    const int w = (RF_USED - c0) < STG_C ? (RF_USED - c0) : STG_C;
+    if (live)
+#pragma unroll
+      for (int j = 0; j < STG_C; ++j)
+        if (j < w && (j & 1) == role) stage[rr * STG_LD + j] = ref_slot(R, ctrl, c0 + j);
+    __syncthreads();
+    for (int idx = tid; idx < nb * w; idx += PRE_T) {
+      const int q = idx / w, j = idx - q * w;
+      ref[(r0 + q) * RF_LD + c0 + j] = stage[q * STG_LD + j];
+    }
+    __syncthreads();
+  }
 #endif
 }
 
@@ -964,7 +971,7 @@ extern "C" int qloco_rt_tick(int64_t batch, void *workspace, const double *gait_
   a.sched = sched;
   rt::aaa_inv_mod(a.aaa_inv_mod);
   const hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(rt::rt_pre_kernel, dim3((unsigned)((batch + rt::PRE_T - 1) / rt::PRE_T)),
+  hipLaunchKernelGGL(rt::rt_pre_kernel, dim3((unsigned)((batch + rt::PRE_R - 1) / rt::PRE_R)),
                      dim3(rt::PRE_T), 0, s, a);
   QLOCO_HIP_CHECK(hipGetLastError(), "rt_pre_kernel launch");
   const rt::Ws L = rt::layout(batch);
