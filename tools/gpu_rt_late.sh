@@ -1,3 +1,8 @@
+#!/bin/bash
+# rt tick time vs walking time (warm-up 150 / 1000 / 1500 ticks), product
+# library against tools/_var/prev (build it with tools/variant_lib.py from
+# the tree to compare against, and drop ./tools/_var from .gpurunignore for
+# the call).
 set -o pipefail
 mkdir -p gpurun_out/late
 for W in 150 1000 1500; do
