@@ -149,3 +149,22 @@ def test_cpp_shim_exports_reference_classes():
                 "qloco::Kinematicclass::Forward_kinematics_g",
                 "qloco::Kinematicclass::Inverse_kinematics_g"):
         assert sym in out, sym
+
+
+def test_rt_servo_support_argument_validation_without_device_work():
+    """the rt tick, servo block and contact-phase entry points reject bad
+    calls (and accept empty batches) before any device work"""
+    L = _lib.lib()
+    assert L.qloco_rt_workspace_bytes(-1) == -1
+    assert L.qloco_servo_workspace_bytes(-1) == -1
+    # the rt node state is allocated in whole 64-robot tiles (551 doubles each)
+    assert L.qloco_rt_workspace_bytes(1) >= 8 * 551 * 64
+    assert L.qloco_rt_workspace_bytes(65) > L.qloco_rt_workspace_bytes(64)
+    assert L.qloco_rt_init(-1, None, None) == 100
+    assert L.qloco_rt_init(0, None, None) == 0
+    assert L.qloco_rt_tick(-1, *([None] * 8)) == 100
+    assert L.qloco_rt_tick(0, *([None] * 8)) == 0
+    assert L.qloco_rt_tick(4, *([None] * 8)) == 100
+    assert L.qloco_support_phase(-1, *([None] * 8)) == 100
+    assert L.qloco_support_phase(0, *([None] * 8)) == 0
+    assert L.qloco_support_phase(4, *([None] * 8)) == 100
