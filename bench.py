@@ -79,6 +79,88 @@ def _config_tag(N, gait, B):
     return tags.get((N, gait, B), "")
 
 
+def usable_cores():
+    """Host cores this process may actually run on: the affinity mask, capped by
+    the cgroup CPU quota when one is set (the GPU box gives each GPU a CPU share
+    smaller than the machine; os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(-(-int(quota) // int(period)))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N ranks through
+    torch.distributed.run as a CHILD process (this process never touches the
+    GPU, so nothing is exec'd from a GPU-initialised process), relay rank 0's
+    JSON line and exit with the launcher's status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    for ln in lines:
+        print(ln, flush=True)
+    if p.returncode == 0 and len(lines) != 1:
+        print("bench.py: expected one JSON line from rank 0, got %d" % len(lines), file=sys.stderr)
+        return 1
+    return p.returncode
+
+
+def dist_selftest(args, rank, world):
+    """CPU check of the multi-rank launch path (tests/test_bench_launch.py): gloo
+    process group, the world size the launcher was asked for, and the step's one
+    collective (ForceGather) -- no GPU, no solve."""
+    import torch
+    import torch.distributed as dist
+    if "MASTER_ADDR" in os.environ:
+        dist.init_process_group("gloo")
+    else:  # --gpus 1 without a launcher
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % _free_port(),
+                                rank=0, world_size=1)
+    from quadrupedal_loco_amd.dist import ForceGather, shard_range
+    B = 8
+    first, _ = shard_range(B, rank)
+    u0 = (torch.arange(B * 12, dtype=torch.float32).reshape(B, 12) + 12 * first)
+    out = ForceGather(B)(u0)
+    ok = bool(torch.equal(out, torch.arange(world * B * 12, dtype=torch.float32)
+                          .reshape(world * B, 12)))
+    t = torch.tensor([1.0 if ok else 0.0])
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        print(json.dumps({"selftest": "dist-launch", "n_gpus": world, "requested": args.gpus,
+                          "allgather_ok": bool(t.item() == 1.0)}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,7 +171,8 @@ def main():
     ap.add_argument("--gait", default="trot")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: every usable host core)")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--overlap", action="store_true",
                     help="N > 1: run each step's all-gather under the next solve (double-"
@@ -97,13 +180,29 @@ def main():
                          "the CUs with the solve cost more than it hid (DESIGN.md §7)")
     ap.add_argument("--force-dist", action="store_true",
                     help="testing: run the N > 1 code path (RCCL group, all-gather) at N = 1")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="testing (CPU): launch path + gloo all-gather only, no GPU")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
-    import torch
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:  # no launcher: spawn the ranks ourselves (before any GPU call)
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d" % (os.environ["WORLD_SIZE"], args.gpus),
+              file=sys.stderr)
+        sys.exit(2)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if args.dist_selftest:
+        dist_selftest(args, rank, world)
+        return
+
+    import torch
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -194,6 +293,7 @@ def main():
 
     kern_ms = np.array([ev_s[i].elapsed_time(ev_k[i]) for i in range(K)])
     step_ms = np.array([ev_s[i].elapsed_time(ev_e[i]) for i in range(K)])
+    gather_ms = np.array([ev_k[i].elapsed_time(ev_e[i]) for i in range(K)])
 
     # per-instance stats of the solved batch (identical every step)
     status = out.status.cpu().numpy()
@@ -231,6 +331,8 @@ def main():
         "p99_batch_us": round(float(np.percentile(step_ms, 99)) * 1e3, 2),
         "p50_batch_us": round(float(np.percentile(step_ms, 50)) * 1e3, 2),
         "kernel_us_avg": round(float(kern_ms.mean()) * 1e3, 2),
+        "allgather_us_avg": (round(float(gather_ms.mean()) * 1e3, 2)
+                             if gather is not None and not overlap else None),
         "admm_iters_p50_p99": [int(np.percentile(iters, 50)), int(np.percentile(iters, 99))],
         "status_ok_frac": float(np.mean(status == 0)),
         "roofline": {
@@ -265,12 +367,13 @@ def main():
 
 def cpu_baseline(N, gait, seconds, threads):
     """CPU-A baseline: the oracle's literal ConvexMpc build + OSQP-algorithm
-    ADMM restatement (double, full 12N-variable QP) on host threads, over a
-    bounded sample of the same synthetic workload."""
+    ADMM restatement (double, full 12N-variable QP) on host threads -- one per
+    usable host core unless --cpu-threads says otherwise -- over a bounded
+    sample of the same synthetic workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes as C
     import oracle_lib as O
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads = threads if threads > 0 else usable_cores()
     sp = O.srbd_spec(N=N)
     st = O.admm_settings()
     g = {"trot": 0, "pace": 1, "mixed": 2, "stance": 3}.get(gait, 0)
@@ -288,6 +391,7 @@ def cpu_baseline(N, gait, seconds, threads):
     count = int(max(probe, min(2_000_000, probe * seconds / max(tp, 1e-6))))
     t = run(count)
     return {"value": round(count / t, 1), "unit": "solves/s", "cores": threads,
+            "host_cores": os.cpu_count(), "cpu_model": cpu_model(),
             "kind": "port",
             "sample": "%d instances of the same workload (first %d of the seed), oracle CPU-A "
                       "(literal dense ConvexMpc build + OSQP-algorithm ADMM, fp64), %.1f s"

@@ -19,7 +19,7 @@
  *
  * Errors: every function returns a qloco_status (0 = success).  Per-instance
  * solver outcomes go to the status[] arrays, mirroring QPBaseClass::solveQP
- * (QPBaseClass.cpp:200-227), which reports failure only through NaN in X.
+ * (QPBaseClass.cpp:126-152), which reports failure only through NaN in X.
  */
 #ifndef QLOCO_H
 #define QLOCO_H
@@ -77,7 +77,8 @@ typedef struct qloco_srbd_spec {
   int32_t max_iter, check_termination, scaling, adaptive_rho, adaptive_rho_interval;
   float adaptive_rho_tolerance;
   int32_t warm_start;        /* 1: read x/y warm start from d_warm (OSQP warm_start) */
-  int32_t polish;            /* 1: OSQP-style solution polishing after ADMM          */
+  int32_t polish;            /* must be 0: OSQP polishing is not implemented (the    */
+                             /* reference leaves it off); 1 -> QLOCO_ERR_ARG         */
   int32_t reserved[6];
 } qloco_srbd_spec;
 

@@ -56,6 +56,7 @@ class DeviceArena {
   DeviceArena(const DeviceArena &) = delete;
   DeviceArena &operator=(const DeviceArena &) = delete;
   void *alloc(size_t bytes);        // persistent block, freed with the arena
+  void release(void *p);            // free one block early (no-op on nullptr)
   void upload(void *dev, const void *host, size_t bytes);
   void download(void *host, const void *dev, size_t bytes);
   void sync();
@@ -88,6 +89,7 @@ class QPsolverGpu {
 
  private:
   int n_ = 0, p_ = 0, m_ = 0, cap_ = 0, max_batch_;
+  int an_ = 0, ap_ = 0, am_ = 0;  // sizes the current device blocks were allocated for
   DeviceArena arena_;
   double *dG_ = nullptr, *dg0_ = nullptr, *dCE_ = nullptr, *dce0_ = nullptr, *dCI_ = nullptr,
          *dci0_ = nullptr, *dX_ = nullptr, *df_ = nullptr;

@@ -56,7 +56,7 @@ struct SrbdArgs {
   float rho, sigma, alpha, eps_abs, eps_rel;
   int max_iter, check_termination, scaling, adaptive_rho, rho_interval;
   float rho_tol;
-  int warm_start, polish;
+  int warm_start;
   // instances with nlegs outside [leg_lo, leg_hi] belong to the other
   // launch of a split batch (qloco_srbd_solve_ex) and are skipped
   int leg_lo, leg_hi;
@@ -593,11 +593,17 @@ __device__ unsigned int g_phase[1 << 20];
 // waves per SIMD the tail of long instances dominates and more registers per
 // wave (no scratch round trips) beat the third resident wave.  Measured on
 // Go1 trot N = 10: B = 4096 307 vs 314 us, B = 8192 539 vs 505 us.
-constexpr int64_t kSmallBatch = 6144;
+#ifndef QLOCO_SRBD_NUM_VGPR_ATTR  // experiments: force a VGPR budget
+#define QLOCO_SRBD_NUM_VGPR_ATTR
+#endif
+#ifndef QLOCO_SMALL_BATCH
+#define QLOCO_SMALL_BATCH 6144
+#endif
+constexpr int64_t kSmallBatch = QLOCO_SMALL_BATCH;
 
 template <int W, int WPE>
 __global__ __launch_bounds__(64 * W)
-__attribute__((amdgpu_waves_per_eu(WPE)))
+__attribute__((amdgpu_waves_per_eu(WPE))) QLOCO_SRBD_NUM_VGPR_ATTR
 void srbd_admm_kernel(const SrbdArgs a) {
   constexpr int NC = 64 * W, NQ = 16 * W;
   __shared__ __attribute__((aligned(16))) SrbdLds<W> S;
@@ -1284,6 +1290,10 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   if (!x0 || !x_ref || !feet || !contacts || !u0) return QLOCO_ERR_ARG;
   if (spec->warm_start && !warm) return QLOCO_ERR_ARG;
   if (spec->mass <= 0.0f || spec->dt <= 0.0f) return QLOCO_ERR_ARG;
+  // OSQP polishing (off in OSQP's defaults and in the reference, which never
+  // enables it, A1RobotControl.cpp:558-559) is not implemented: refuse rather
+  // than return unpolished iterates as if polished
+  if (spec->polish) return QLOCO_ERR_ARG;
   SrbdArgs a;
   memset(&a, 0, sizeof(a));
   a.N = spec->horizon;
@@ -1310,7 +1320,6 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   a.rho_interval = spec->adaptive_rho_interval;
   a.rho_tol = spec->adaptive_rho_tolerance;
   a.warm_start = spec->warm_start;
-  a.polish = spec->polish;
   a.batch = batch;
   a.x0 = x0;
   a.xref = x_ref;

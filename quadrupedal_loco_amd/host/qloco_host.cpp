@@ -47,6 +47,16 @@ void *DeviceArena::alloc(size_t bytes) {
   blocks_.push_back(p);
   return p;
 }
+void DeviceArena::release(void *p) {
+  if (!p) return;
+  for (size_t i = 0; i < blocks_.size(); ++i)
+    if (blocks_[i] == p) {
+      (void)hipFree(p);
+      blocks_[i] = blocks_.back();
+      blocks_.pop_back();
+      return;
+    }
+}
 void DeviceArena::upload(void *dev, const void *host, size_t bytes) {
   if (bytes) hip_ok(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, (hipStream_t)stream_), "upload");
 }
@@ -71,11 +81,20 @@ void QPsolverGpu::resize(const int &nVar, const int &nEq, const int &nIneq) {
   n_ = nVar;
   p_ = nEq;
   m_ = nIneq;
-  cap_ = 0;  // re-allocate at the next solve
 }
 
+// Device blocks are reused while the batch and the (n, p, m) of the last
+// resize fit the sizes they were allocated for; otherwise the old blocks are
+// freed before the new ones are allocated (repeated resizeQP calls or a
+// growing batch do not accumulate device memory).
 void QPsolverGpu::ensure(int batch) {
-  if (batch <= cap_) return;
+  if (batch <= cap_ && n_ <= an_ && p_ <= ap_ && m_ <= am_) return;
+  for (void *p : {(void *)dG_, (void *)dg0_, (void *)dCE_, (void *)dce0_, (void *)dCI_,
+                  (void *)dci0_, (void *)dX_, (void *)df_, (void *)dst_, (void *)dit_})
+    arena_.release(p);
+  dG_ = dg0_ = dCE_ = dce0_ = dCI_ = dci0_ = dX_ = df_ = nullptr;
+  dst_ = dit_ = nullptr;
+  if (batch < cap_) batch = cap_;
   const size_t B = batch;
   dG_ = dalloc<double>(arena_, B * n_ * n_);
   dg0_ = dalloc<double>(arena_, B * n_);
@@ -88,6 +107,9 @@ void QPsolverGpu::ensure(int batch) {
   dst_ = dalloc<int32_t>(arena_, B);
   dit_ = dalloc<int32_t>(arena_, B);
   cap_ = batch;
+  an_ = n_;
+  ap_ = p_;
+  am_ = m_;
 }
 
 void QPsolverGpu::solve_batch(int batch, const double *G, const double *g0, const double *CE,

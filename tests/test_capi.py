@@ -168,3 +168,23 @@ def test_rt_servo_support_argument_validation_without_device_work():
     assert L.qloco_support_phase(-1, *([None] * 8)) == 100
     assert L.qloco_support_phase(0, *([None] * 8)) == 0
     assert L.qloco_support_phase(4, *([None] * 8)) == 100
+    # servo force block (servo.cpp:1052-1243 replacement)
+    fp = qp.force_params()
+    assert L.qloco_servo_init(-1, None, None) == 100
+    assert L.qloco_servo_init(0, None, None) == 0
+    assert L.qloco_servo_init(4, None, None) == 100          # NULL workspace
+    assert L.qloco_servo_force_block(None, 1, *([None] * 22)) == 100
+    assert L.qloco_servo_force_block(C.byref(fp), -1, *([None] * 22)) == 100
+    assert L.qloco_servo_force_block(C.byref(fp), 0, *([None] * 22)) == 0
+    assert L.qloco_servo_force_block(C.byref(fp), 4, *([None] * 22)) == 100
+
+
+def test_srbd_polish_rejected_until_implemented():
+    """OSQP polishing is not implemented: a spec asking for it is refused
+    (QLOCO_ERR_ARG) instead of silently returning unpolished iterates."""
+    L = _lib.lib()
+    sp = srbd.default_spec(polish=1)
+    dummy = [C.c_void_p(16)] * 5  # never dereferenced: rejected before any device work
+    assert L.qloco_srbd_solve(C.byref(sp), 4, *dummy, None, None, None, None, None, None) == 100
+    assert L.qloco_srbd_solve_ex(C.byref(sp), 4, *dummy, None, None, None, None, None, None,
+                                 0, None) == 100

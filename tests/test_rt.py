@@ -136,3 +136,26 @@ def test_replay_log_roundtrip_and_oracle_replay(tmp_path):
         f.truncate(1000)
     with pytest.raises(ValueError):
         read_log(path)
+
+
+def test_rt_tick_rejects_bad_messages():
+    """RtNodeBatch.tick validates its message rows before any launch (a wrong
+    dtype / shape / layout / device would make rt_pre_kernel read out of
+    bounds); checked on CPU with a node object that never touched a GPU."""
+    torch = pytest.importorskip("torch")
+    from quadrupedal_loco_amd import rt
+    node = object.__new__(rt.RtNodeBatch)
+    node.batch, node.device = 4, torch.device("cuda", 0)
+    good_g = torch.zeros((4, rt.GAIT_LEN), dtype=torch.float64)
+    good_c = torch.zeros((4, rt.CTRL_LEN), dtype=torch.float64)
+    bad = [
+        (good_g.float(), good_c, "float64"),                          # dtype
+        (good_g[:, :99].contiguous(), good_c, r"\(4, 100\)"),         # short rows
+        (torch.zeros((4, 200), dtype=torch.float64)[:, ::2], good_c, "non-contiguous"),
+        (good_g.numpy(), good_c, "torch tensor"),                     # host numpy array
+        (good_g, torch.zeros((3, rt.CTRL_LEN), dtype=torch.float64), "ctrl_msg"),
+        (good_g, good_c, "on cpu"),                                   # host tensors
+    ]
+    for g, c, msg in bad:
+        with pytest.raises(ValueError, match=msg):
+            node.tick(g, c)

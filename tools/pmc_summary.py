@@ -1,20 +1,44 @@
-"""Summarise rocprofv3 PMC databases written by tools/gpu_pmc.sh (per-wave averages)."""
+"""Summarise rocprofv3 PMC databases: per dispatch, each counter summed over
+its dimensions (SE / XCD instances), then averaged over the dispatches of the
+matching kernel.  Usage: python tools/pmc_summary.py DIR [KERNEL_SUBSTRING]
+(DIR: a rocprofv3 -d directory, or a parent holding pmc*/ subdirectories)."""
 import collections
 import glob
 import os
 import sqlite3
 import sys
 
-root = sys.argv[1]
-kern = sys.argv[2] if len(sys.argv) > 2 else "srbd_admm"
-for d in sorted(glob.glob(os.path.join(root, "pmc*_*"))):
+
+def summarise(d, kern):
     dbs = glob.glob(os.path.join(d, "**", "*.db"), recursive=True)
     if not dbs:
-        continue
+        return None
     cur = sqlite3.connect(dbs[0]).cursor()
-    rows = cur.execute("select kernel_name, counter_name, value from counters_collection").fetchall()
-    agg = collections.defaultdict(list)
-    for k, c, v in rows:
+    rows = cur.execute("select dispatch_id, kernel_name, counter_name, value, duration "
+                       "from counters_collection").fetchall()
+    per = collections.defaultdict(float)
+    dur = {}
+    for disp, k, c, v, du in rows:
         if kern in str(k):
-            agg[c].append(v)
-    print(os.path.basename(d), {c: round(sum(v) / len(v)) for c, v in sorted(agg.items())})
+            per[(disp, c)] += v
+            dur[disp] = du
+    agg = collections.defaultdict(list)
+    for (disp, c), v in per.items():
+        agg[c].append(v)
+    out = {c: sum(v) / len(v) for c, v in sorted(agg.items())}
+    if dur:
+        out["duration_ns"] = sum(dur.values()) / len(dur)
+        out["dispatches"] = len(dur)
+    return out
+
+
+if __name__ == "__main__":
+    root = sys.argv[1]
+    kern = sys.argv[2] if len(sys.argv) > 2 else "srbd_admm"
+    dirs = [root] if glob.glob(os.path.join(root, "*.db")) or glob.glob(
+        os.path.join(root, "*", "*.db")) and not glob.glob(os.path.join(root, "pmc*")) else \
+        sorted(glob.glob(os.path.join(root, "pmc*")))
+    for d in dirs:
+        s = summarise(d, kern)
+        if s:
+            print(os.path.basename(d), {k: round(v) for k, v in s.items()})
