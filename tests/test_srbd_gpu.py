@@ -10,11 +10,14 @@ EiQuadProg, double).  Stated fp32 tolerances:
       tolerance: in the QP's near-flat directions -- internal forces between
       stance feet, curvature = R = 2e-7 -- fp32 and fp64 runs of the same
       algorithm land at different eps-optimal points);
+  * the quantities the cost sees (per-step net wrench, predicted state
+    trajectory in the Q-norm) vs that restatement, vs the exact optimum at
+    eps 1e-6 and vs the literal full 12N-variable OSQP restatement, with the
+    bounds stated in each test (the fp64 envelopes they come from are in
+    DESIGN.md §6);
   * vs the exact optimum of the reference's literal 12N-variable QP
-    (EiQuadProg restatement): objective gap in [-1e-3, 0.1] * max(1, |f*|)
-    -- the band the fp64 ADMM restatement itself lands in at OSQP's default
-    eps_abs = eps_rel = 1e-3; a slightly negative gap is the eps-sized
-    constraint violation ADMM allows -- and violation <= 0.25 N;
+    (EiQuadProg restatement): objective gap within 1e-3 of the fp64
+    restatement's own gap and violation <= 0.25 N;
   * integer structure (stance enumeration -> variable count) bit-exact,
     checked through the exactly-zero swing forces.
 """
@@ -98,6 +101,13 @@ def test_srbd_matches_admm_restatement(N, B, gait):
 
 @pytest.mark.parametrize("N,B,gait", [(10, 24, "trot"), (10, 16, "mixed")])
 def test_srbd_vs_exact_optimum(N, B, gait):
+    """Objective gap to the exact optimum f* of the literal 12N-variable QP:
+    within 1e-3 of the gap the fp64 OSQP-algorithm restatement itself lands
+    at (OSQP's default eps stops anywhere in an eps-ball; measured fp64 gaps
+    on configs 2-5 shapes span [-2.1e-3, 0.137] of max(1, |f*|), measured
+    GPU - fp64 differences <= 3.6e-4), inside that envelope with margin, and
+    constraint violation <= 0.25 N.  (The former eps-1e-6 check is
+    test_srbd_tight_eps_wrench_vs_exact.)"""
     (x0, xr, ft, ct), r = _solve(N, B, gait)
     sp = O.srbd_spec(N=N)
     for b in range(B):
@@ -105,23 +115,14 @@ def test_srbd_vs_exact_optimum(N, B, gait):
         xe, st, _ = inst.exact()
         assert st == 0
         fe = inst.obj(xe)
+        sc = max(1.0, abs(fe))
         u = r["u"][b].astype(np.float64)
-        gap = (inst.obj(u) - fe) / max(1.0, abs(fe))
-        assert -1e-3 <= gap <= 0.1, (b, gap)
+        gap = (inst.obj(u) - fe) / sc
+        gap64 = (inst.obj(inst.admm_reduced()[0]) - fe) / sc
+        assert abs(gap - gap64) <= 1e-3, (b, gap, gap64)
+        assert -2.5e-3 <= gap <= 0.15, (b, gap)
         assert inst.violation(u) <= 0.25, (b, inst.violation(u))
         assert abs(r["obj"][b] - inst.obj(u)) <= 1e-3 * max(1.0, abs(inst.obj(u)))
-
-
-def test_srbd_tight_tolerance_reaches_exact_optimum():
-    N, B = 10, 8
-    (x0, xr, ft, ct), r = _solve(N, B, "trot", eps_abs=1e-6, eps_rel=1e-6, max_iter=20000)
-    sp = O.srbd_spec(N=N)
-    for b in range(B):
-        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
-        xe, _, _ = inst.exact()
-        fe = inst.obj(xe)
-        u = r["u"][b].astype(np.float64)
-        assert (inst.obj(u) - fe) <= 1e-3 * max(1.0, abs(fe)), (b, inst.obj(u), fe)
 
 
 def test_srbd_body_frame_output_and_determinism():
