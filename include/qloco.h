@@ -326,6 +326,43 @@ int qloco_support_phase(int64_t batch, const double *ts, const double *tx, const
                         const int32_t *t_end_footstep, int32_t *bjxx, int32_t *bjx1,
                         int32_t *right_support, void *stream);
 
+/* ====================================================================== */
+/* 9. A1 single-step force QP, batched (fp64)                               */
+/*    replaces the stance_leg_control_type == 0 branch of                  */
+/*    A1RobotControl::compute_grf (unitree_ros/a1_cpp_open_source/src/     */
+/*    A1RobotControl.cpp:383-450; constructor :8-49): root_acc from PD      */
+/*    gains, H = R I + inv' Q inv, g = -inv' Q root_acc, 20-row friction    */
+/*    pyramid / normal-force block, cold OSQP solve with default settings,  */
+/*    forces rotated into the body frame.                                   */
+/* ====================================================================== */
+typedef struct qloco_a1_params {
+  double kp_linear[3], kd_linear[3], kp_angular[3], kd_angular[3]; /* A1CtrlStates.h:123-126 */
+  double robot_mass;                                                /* A1CtrlStates.h:39 */
+  double q_diag[6];  /* Q (A1RobotControl.cpp:12) */
+  double r;          /* R = 1e-3 (:13) */
+  double mu;         /* 0.7 (:14) */
+  double f_min, f_max; /* 0 / 180 (:15-16) */
+  /* OSQP settings (defaults = OsqpEigen's, i.e. OSQP v0.6 defaults) */
+  double rho, sigma, alpha, eps_abs, eps_rel, adaptive_rho_tolerance;
+  int32_t max_iter, check_termination, scaling, adaptive_rho, adaptive_rho_interval;
+  int32_t reserved[3];
+} qloco_a1_params;
+void qloco_a1_params_default(qloco_a1_params *p);
+/* Per-robot state record, double[QLOCO_A1_STATE_LEN] (A1CtrlStates fields):
+ *   [0:3] root_pos  [3:6] root_pos_d  [6:9] root_euler  [9:12] root_euler_d
+ *   [12:15] root_lin_vel (world)  [15:18] root_lin_vel_d (body)
+ *   [18:21] root_ang_vel (world)  [21:24] root_ang_vel_d (body)
+ *   [24:33] root_rot_mat  [33:42] root_rot_mat_z  (3x3 col-major)
+ *   [42:54] foot_pos_abs (3x4 col-major, legs FL, FR, RL, RR)
+ * contacts[B*4] uint8.  Outputs: forces_body[B*12] (foot_forces_grf, 3x4
+ * col-major) required; qp_solution[B*12] (world frame), status[B],
+ * iters[B], rho_updates[B], obj[B] optional (NULL). */
+#define QLOCO_A1_STATE_LEN 54
+int qloco_a1_qp_solve(const qloco_a1_params *prm, int64_t batch, const double *state,
+                      const uint8_t *contacts, double *forces_body, double *qp_solution,
+                      int32_t *status, int32_t *iters, int32_t *rho_updates, double *obj,
+                      void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -263,6 +263,29 @@ int qo_exact_solve(int n, int m, const double *P, const double *q, const double 
                    const double *l, const double *u, double *x, int *iters);
 
 /* ------------------------------------------------------------------ */
+/* A1 single-step force QP: A1RobotControl::compute_grf with            */
+/* stance_leg_control_type == 0 (A1RobotControl.cpp:383-450, ctor :8-49) */
+/* (a1_qp.c).  12 variables (legs FL, FR, RL, RR), 20 rows, OSQP.        */
+/* ------------------------------------------------------------------ */
+#define QO_A1_STATE_LEN 54
+typedef struct {
+  double kp_linear[3], kd_linear[3], kp_angular[3], kd_angular[3];
+  double robot_mass;
+  double q_diag[6], r, mu, f_min, f_max;
+} qo_a1_params;
+void qo_a1_params_default(qo_a1_params *p);
+/* the QP the branch hands to OSQP: H (12x12), g, linearMatrix A (20x12,
+ * col-major), bounds; root_acc (6) as computed at :384-397 */
+void qo_a1_qp_build(const qo_a1_params *p, const double *state, const uint8_t contacts[4],
+                    double root_acc[6], double H[144], double g[12], double A[240],
+                    double l[20], double u[20]);
+/* build + cold OSQP-algorithm solve + rotation into the body frame
+ * (:445-449).  x (world-frame QPSolution, 12) and info may be NULL. */
+int qo_a1_compute_grf(const qo_a1_params *p, const qo_admm_settings *st, const double *state,
+                      const uint8_t contacts[4], double forces_body[12], double x[12],
+                      qo_admm_info *info);
+
+/* ------------------------------------------------------------------ */
 /* Deterministic synthetic instances.                   */
 /* Restated independently from the product's generator; tests compare. */
 /* ------------------------------------------------------------------ */

@@ -35,6 +35,20 @@ class ForceParams(C.Structure):
     _fields_ = [(k, C.c_double) for k in ("mass", "alpha", "beta", "gamma", "fz_max", "mu")]
 
 
+class A1Params(C.Structure):
+    """Mirror of `qloco_a1_params`."""
+    _fields_ = [("kp_linear", C.c_double * 3), ("kd_linear", C.c_double * 3),
+                ("kp_angular", C.c_double * 3), ("kd_angular", C.c_double * 3),
+                ("robot_mass", C.c_double), ("q_diag", C.c_double * 6), ("r", C.c_double),
+                ("mu", C.c_double), ("f_min", C.c_double), ("f_max", C.c_double),
+                ("rho", C.c_double), ("sigma", C.c_double), ("alpha", C.c_double),
+                ("eps_abs", C.c_double), ("eps_rel", C.c_double),
+                ("adaptive_rho_tolerance", C.c_double),
+                ("max_iter", C.c_int32), ("check_termination", C.c_int32),
+                ("scaling", C.c_int32), ("adaptive_rho", C.c_int32),
+                ("adaptive_rho_interval", C.c_int32), ("reserved", C.c_int32 * 3)]
+
+
 vp = C.c_void_p
 i64 = C.c_int64
 i32 = C.c_int32
@@ -72,6 +86,8 @@ SIGNATURES = {
     "qloco_servo_init": (C.c_int, [i64, vp, vp]),
     "qloco_servo_force_block": (C.c_int, [C.POINTER(ForceParams), i64] + [vp] * 22),
     "qloco_support_phase": (C.c_int, [i64] + [vp] * 8),
+    "qloco_a1_params_default": (None, [C.POINTER(A1Params)]),
+    "qloco_a1_qp_solve": (C.c_int, [C.POINTER(A1Params), i64] + [vp] * 9),
 }
 
 

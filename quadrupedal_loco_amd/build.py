@@ -28,6 +28,7 @@ SOURCES = [
     "qloco_body.hip",
     "qloco_rt.hip",
     "qloco_servo.hip",
+    "qloco_a1qp.hip",
     "qloco_gen.cpp",
 ]
 # per-file extra flags: the fp64 active-set kernel keeps the restatement's
@@ -38,7 +39,7 @@ SOURCES = [
 # Gauss-Jordan updates are written with explicit float2 ops).  Its pivot
 # loops are unrolled in full (static register per pivot column); the two-wave
 # inverse's body exceeds the default pragma-unroll budget, so it is raised.
-EXTRA = {"qloco_gi.hip": ["-ffp-contract=off"], "qloco_force.hip": ["-ffp-contract=off"],
+EXTRA = {"qloco_a1qp.hip": ["-ffp-contract=off"], "qloco_gi.hip": ["-ffp-contract=off"], "qloco_force.hip": ["-ffp-contract=off"],
          "qloco_body.hip": ["-ffp-contract=off"], "qloco_rt.hip": ["-ffp-contract=off"], "qloco_servo.hip": ["-ffp-contract=off"], "qloco_kin.hip": ["-ffp-contract=off"], "qloco_srbd.hip": ["-fno-slp-vectorize", "-mllvm", "-pragma-unroll-threshold=200000"]}
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC]
@@ -54,7 +55,7 @@ def _needs(obj, deps):
 def build(verbose=False, jobs=8):
     os.makedirs(OBJDIR, exist_ok=True)
     headers = [os.path.join(INCLUDE, "qloco.h")] + [
-        os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+        os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h", ".inc"))]
     cmds, objs = [], []
     for src in SOURCES:
         path = os.path.join(CSRC, src)

@@ -48,6 +48,13 @@ class AdmmInfo(C.Structure):
                 ("rho_final", C.c_double)]
 
 
+class A1Params(C.Structure):
+    _fields_ = [("kp_linear", C.c_double * 3), ("kd_linear", C.c_double * 3),
+                ("kp_angular", C.c_double * 3), ("kd_angular", C.c_double * 3),
+                ("robot_mass", C.c_double), ("q_diag", C.c_double * 6), ("r", C.c_double),
+                ("mu", C.c_double), ("f_min", C.c_double), ("f_max", C.c_double)]
+
+
 class ForceParams(C.Structure):
     _fields_ = [(k, C.c_double) for k in ("mass", "alpha", "beta", "gamma", "fz_max", "mu")]
 
@@ -148,6 +155,11 @@ def lib():
         L.qo_rt_tick_n.argtypes = [C.c_void_p, C.c_int64] + [C.c_void_p] * 6
         L.qo_inv4.argtypes = [dp, dp]
         L.qo_support_phase.argtypes = [C.c_int64] + [C.c_void_p] * 7
+        L.qo_a1_params_default.argtypes = [C.POINTER(A1Params)]
+        L.qo_a1_qp_build.argtypes = [C.POINTER(A1Params), dp, u8p, dp, dp, dp, dp, dp, dp]
+        L.qo_a1_compute_grf.restype = C.c_int
+        L.qo_a1_compute_grf.argtypes = [C.POINTER(A1Params), C.POINTER(AdmmSettings), dp, u8p,
+                                        dp, dp, C.POINTER(AdmmInfo)]
         _lib = L
     return _lib
 
@@ -392,3 +404,33 @@ def support_phase(ts, tx, t_int, t_end):
                            t_end.ctypes.data, out[0].ctypes.data, out[1].ctypes.data,
                            out[2].ctypes.data)
     return out[0], out[1], out[2]
+
+
+# ---- A1 single-step QP (oracle/a1_qp.c)
+def a1_params():
+    p = A1Params()
+    lib().qo_a1_params_default(C.byref(p))
+    return p
+
+
+def a1_build(state, contacts, params=None):
+    """(root_acc, H, g, A, l, u) of the A1 QP branch, column-major A (20x12)."""
+    p = params or a1_params()
+    s = np.ascontiguousarray(state, np.float64)
+    c = np.ascontiguousarray(contacts, np.uint8)
+    acc, H, g = np.zeros(6), np.zeros(144), np.zeros(12)
+    A, l, u = np.zeros(240), np.zeros(20), np.zeros(20)
+    lib().qo_a1_qp_build(C.byref(p), P(s), P(c, C.c_uint8), P(acc), P(H), P(g), P(A), P(l), P(u))
+    return acc, H.reshape(12, 12).T.copy(), g, A.reshape(12, 20).T.copy(), l, u
+
+
+def a1_compute_grf(state, contacts, params=None, **admm):
+    """qo_a1_compute_grf: (forces_body (12,), x (12,), AdmmInfo)."""
+    p = params or a1_params()
+    st = admm_settings(**admm)
+    s = np.ascontiguousarray(state, np.float64)
+    c = np.ascontiguousarray(contacts, np.uint8)
+    f, x, info = np.zeros(12), np.zeros(12), AdmmInfo()
+    lib().qo_a1_compute_grf(C.byref(p), C.byref(st), P(s), P(c, C.c_uint8), P(f), P(x),
+                            C.byref(info))
+    return f, x, info
