@@ -76,11 +76,28 @@ typedef struct qloco_srbd_spec {
   float rho, sigma, alpha, eps_abs, eps_rel;
   int32_t max_iter, check_termination, scaling, adaptive_rho, adaptive_rho_interval;
   float adaptive_rho_tolerance;
-  int32_t warm_start;        /* 1: read x/y warm start from d_warm (OSQP warm_start) */
+  int32_t warm_start;        /* 0: cold start every call                            */
+                             /* 1: osqp_warm_start from the unscaled x|y in warm    */
+                             /*    (B*32N floats, in/out)                           */
+                             /* 2: persistent solver, the reference's member        */
+                             /*    OsqpEigen::Solver (A1RobotControl.cpp:556-578):  */
+                             /*    warm = B*QLOCO_SRBD_PERSIST_LEN(N) floats, zeroed */
+                             /*    before the first call; see DESIGN.md §3          */
   int32_t polish;            /* must be 0: OSQP polishing is not implemented (the    */
                              /* reference leaves it off); 1 -> QLOCO_ERR_ARG         */
   int32_t reserved[6];
 } qloco_srbd_spec;
+
+/* Per-instance record of the persistent solver (spec.warm_start == 2),
+ * floats, full index (variable 12k+3i+c, constraint row 20k+5i+r):
+ *   [0,12N) scaled x  [12N,32N) scaled z  [32N,52N) scaled y
+ *   [52N,64N) unscaled x  [64N,84N) unscaled y  [84N,96N) unscaled q
+ *   [96N,100N) contact flags  [100N] rho  [100N+1] 1 after the first call.
+ * Same stance set as the last call: OSQP's update path (osqp_update_P /
+ * _lin_cost / _bounds + solve: Ruiz on the new P with the previous q in the
+ * cost scale, adapted rho kept, scaled iterates carried); a changed stance
+ * set re-initialises (settings rho) warm-started from the last solution. */
+#define QLOCO_SRBD_PERSIST_LEN(N) (100 * (N) + 4)
 
 /* Go1 SRBD constants + OSQP default settings. */
 void qloco_srbd_spec_default(qloco_srbd_spec *spec);

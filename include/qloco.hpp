@@ -187,6 +187,11 @@ class PRMPCClass {
 // batched fused build + OSQP-algorithm ADMM runs on the GPU, and the forces
 // come back in the body frame (root_rot_mat' u, :596-599).  A leg whose
 // solution is NaN keeps its previous output (the reference's isnan guard).
+// Like the reference's member OsqpEigen::Solver (A1RobotControl.h:67, set up
+// once with warm start on, then update* + solve every tick, :556-578), each
+// robot's solver persists across compute_grf calls (spec.warm_start = 2, the
+// per-robot record on the device); reset() forgets it.  Pass a spec with
+// warm_start = 0 for independent cold solves.
 struct A1MpcState {                // the A1CtrlStates fields compute_grf reads
   double root_euler[3], root_pos[3], root_ang_vel[3], root_lin_vel[3];
   double root_rot_mat[9];          // col-major; used for root_lin_vel_d_world
@@ -203,13 +208,43 @@ class ConvexMpcBatch {
   // device-resident form (inputs already in HBM): thin wrapper of qloco_srbd_solve_ex
   void solve_device(const float *x0, const float *x_ref, const float *feet,
                     const uint8_t *contacts, float *u0, int32_t *status, int32_t *iters);
+  void reset();  // fresh solvers (the next call sets each one up again)
   qloco_srbd_spec spec;
   std::vector<int32_t> status, iters;
 
  private:
   int batch_;
   DeviceArena arena_;
-  float *d_x0_, *d_xr_, *d_feet_, *d_u0_;
+  float *d_x0_, *d_xr_, *d_feet_, *d_u0_, *d_rec_ = nullptr;
+  uint8_t *d_ct_;
+  int32_t *d_st_, *d_it_;
+};
+
+// ------------------------------------------------------------------------
+// A1RobotControl::compute_grf, QP branch (stance_leg_control_type == 0,
+// A1RobotControl.cpp:383-450) over B robots: the A1CtrlStates fields it
+// reads, the weights / gains of qloco_a1_params, one cold OSQP solve per
+// robot (fp64, qloco_a1_qp_solve), forces in the body frame.
+struct A1QpState {
+  double root_pos[3], root_pos_d[3], root_euler[3], root_euler_d[3];
+  double root_lin_vel[3], root_lin_vel_d[3], root_ang_vel[3], root_ang_vel_d[3];
+  double root_rot_mat[9], root_rot_mat_z[9];  // col-major
+  double foot_pos_abs[12];                    // 3x4 col-major, legs FL, FR, RL, RR
+  bool contacts[4];
+};
+
+class A1QpBatch {
+ public:
+  A1QpBatch(int batch, const qloco_a1_params *params = nullptr);
+  // foot_forces_grf: B * 12 (3x4 col-major per robot)
+  void compute_grf(const A1QpState *states, double *foot_forces_grf);
+  qloco_a1_params params;
+  std::vector<int32_t> status, iters;
+
+ private:
+  int batch_;
+  DeviceArena arena_;
+  double *d_state_, *d_forces_;
   uint8_t *d_ct_;
   int32_t *d_st_, *d_it_;
 };

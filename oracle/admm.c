@@ -240,6 +240,17 @@ static void scale_data(admm_ws *w, int iters) {
 int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P0, const double *q0,
                   const double *A0, const double *l0, const double *u0, double *xo, double *yo,
                   qo_admm_info *info) {
+  qo_admm_init in;
+  memset(&in, 0, sizeof(in));
+  in.mode = st->warm_start ? QO_ADMM_WARM : QO_ADMM_COLD;
+  in.x = xo;
+  in.y = yo;
+  return qo_admm_solve_ex(st, n, m, P0, q0, A0, l0, u0, &in, NULL, xo, yo, info);
+}
+
+int qo_admm_solve_ex(const qo_admm_settings *st, int n, int m, const double *P0, const double *q0,
+                     const double *A0, const double *l0, const double *u0, const qo_admm_init *in,
+                     qo_admm_state *out, double *xo, double *yo, qo_admm_info *info) {
   admm_ws W, *w = &W;
   memset(w, 0, sizeof(W));
   w->n = n; w->m = m;
@@ -266,12 +277,25 @@ int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P0, co
   double *tm = (double *)calloc(m > n ? m : n, sizeof(double));
 
   w->sigma = st->sigma;
-  w->rho = st->rho;
+  /* QO_ADMM_RESUME (OSQP's update path, osqp_update_P + osqp_update_lin_cost
+   * + osqp_update_{lower,upper}_bound on a live workspace): scale_data runs
+   * on the new P with the PREVIOUS q still in place (update_P precedes
+   * update_lin_cost), so the cost scale c sees the old gradient; the new q
+   * is then scaled as c * (D q_new); the adapted rho of the last solve stays */
+  const int resume = in && in->mode == QO_ADMM_RESUME;
+  w->rho = resume ? in->rho : st->rho;
+  if (resume && in->q_scale) memcpy(w->q, in->q_scale, sizeof(double) * n);
   if (st->scaling) scale_data(w, st->scaling);
   else {
     w->c = w->cinv = 1.0;
     for (int j = 0; j < n; ++j) w->D[j] = w->Dinv[j] = 1.0;
     for (int i = 0; i < m; ++i) w->E[i] = w->Einv[i] = 1.0;
+  }
+  if (resume && in->q_scale) {
+    for (int j = 0; j < n; ++j) {
+      w->q[j] = w->D[j] * q0[j];
+      w->q[j] *= w->c;
+    }
   }
   csc_build(w);
   set_rho_vec(w);
@@ -280,10 +304,14 @@ int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P0, co
   if (st->adaptive_rho && !interval)
     interval = st->check_termination ? 4 * st->check_termination : 100; /* ADAPTIVE_RHO_FIXED */
 
-  if (st->warm_start) { /* osqp_warm_start: scale x by Dinv, y by Einv*c */
-    for (int j = 0; j < n; ++j) x[j] = xo[j] * w->Dinv[j];
-    for (int i = 0; i < m; ++i) y[i] = yo[i] * w->Einv[i] * w->c;
+  if (in && in->mode == QO_ADMM_WARM) { /* osqp_warm_start: x by Dinv, y by Einv*c, z = A x */
+    for (int j = 0; j < n; ++j) x[j] = in->x[j] * w->Dinv[j];
+    for (int i = 0; i < m; ++i) y[i] = in->y[i] * w->Einv[i] * w->c;
     csc_Ax(w, x, z);
+  } else if (resume) { /* warm_start on a live workspace: the scaled iterates as they are */
+    memcpy(x, in->x, sizeof(double) * n);
+    memcpy(z, in->z, sizeof(double) * m);
+    memcpy(y, in->y, sizeof(double) * m);
   }
 
   int iter, status = QO_MAX_ITER, can_check = 0, rho_updates = 0;
@@ -366,6 +394,12 @@ int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P0, co
     obj += 0.5 * a * x[j] + w->q[j] * x[j];
   }
   obj *= w->cinv;
+  if (out) {
+    memcpy(out->x, x, sizeof(double) * n);
+    memcpy(out->z, z, sizeof(double) * m);
+    memcpy(out->y, y, sizeof(double) * m);
+    out->rho = w->rho;
+  }
   for (int j = 0; j < n; ++j) xo[j] = w->D[j] * x[j];
   if (yo)
     for (int i = 0; i < m; ++i) yo[i] = w->cinv * w->E[i] * y[i];

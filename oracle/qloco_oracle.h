@@ -257,6 +257,46 @@ typedef struct {
 int qo_admm_solve(const qo_admm_settings *st, int n, int m, const double *P,
                   const double *q, const double *A, const double *l,
                   const double *u, double *x, double *y, qo_admm_info *info);
+/* Extended entry: how the iterates start and what survives the solve.
+ *   QO_ADMM_COLD   x = z = y = 0, rho = settings rho (osqp_setup + solve)
+ *   QO_ADMM_WARM   osqp_warm_start from UNSCALED x, y (z = A x)
+ *   QO_ADMM_RESUME OsqpEigen's update*() + solve() on a live solver with
+ *                  warm start on (A1RobotControl.cpp:556-575): scaled x, z, y
+ *                  carried as they are, rho = the adapted rho of the last
+ *                  solve, Ruiz's cost scale computed with q_scale (the
+ *                  previous, unscaled q) before the new q is scaled in.
+ * out (may be NULL): scaled final x (n), z (m), y (m) and rho.            */
+enum { QO_ADMM_COLD = 0, QO_ADMM_WARM = 1, QO_ADMM_RESUME = 2 };
+typedef struct {
+  int mode;
+  const double *x, *z, *y; /* WARM: unscaled x, y; RESUME: scaled x, z, y */
+  double rho;              /* RESUME */
+  const double *q_scale;   /* RESUME: previous unscaled q (NULL = new q) */
+} qo_admm_init;
+typedef struct {
+  double *x, *z, *y;
+  double rho;
+} qo_admm_state;
+int qo_admm_solve_ex(const qo_admm_settings *st, int n, int m, const double *P,
+                     const double *q, const double *A, const double *l, const double *u,
+                     const qo_admm_init *in, qo_admm_state *out, double *x, double *y,
+                     qo_admm_info *info);
+
+/* Persistent SRBD MPC solver: the reference's member OsqpEigen::Solver
+ * (A1RobotControl.h:67) called every control tick (A1RobotControl.cpp:556-
+ * 578) -- restated on the stance-only QP the GPU kernel solves.  Same stance
+ * set as the last call: QO_ADMM_RESUME.  Stance set changed (the reduced
+ * problem's dimensions change): a fresh setup warm-started from the last
+ * unscaled solution, as OsqpEigen's re-initialisation path does
+ * (clearSolver + initSolver + setPrimal/DualVariable).  First call: cold.
+ * The record is full-index (12N variables, 20N rows) like the GPU's:
+ * QO_SRBD_PERSIST_LEN(N) doubles, layout in qloco.h (qloco_srbd_spec). */
+#define QO_SRBD_PERSIST_LEN(N) (100 * (N) + 4)
+int qo_srbd_persist_step(double *rec, const qo_srbd_spec *sp, const qo_admm_settings *st,
+                         const float *x0, const float *x_ref, const float *feet,
+                         int feet_per_step, const uint8_t *contacts, int contacts_per_step,
+                         double *u, qo_admm_info *info);
+
 /* Exact optimum of the same box/row-bounded QP via the EiQuadProg
  * restatement (p = 0, so none of the equality quirks apply).             */
 int qo_exact_solve(int n, int m, const double *P, const double *q, const double *A,

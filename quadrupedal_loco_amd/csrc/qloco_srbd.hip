@@ -661,6 +661,17 @@ void srbd_admm_kernel(const SrbdArgs a) {
     if (t == 0 && a.status) a.status[b] = QLOCO_BAD_SIZE;
     return;
   }
+  // persistent solver (warm_start == 2, A1RobotControl.cpp:556-578): the
+  // record of this instance's last call (layout: QLOCO_SRBD_PERSIST_LEN)
+  const int NP = 100 * N;
+  float *prec = a.warm_start == 2 ? a.warm + b * (int64_t)(NP + 4) : nullptr;
+  bool p_init = false, p_same = false;
+  if (prec) {
+    p_init = prec[NP + 1] > 0.5f;
+    int mism = 0;
+    for (int k = t; k < 4 * N; k += 64 * W) mism |= (prec[96 * N + k] != 0.0f) != (S.ct[k] != 0);
+    p_same = p_init && !__syncthreads_or(mism);
+  }
   int ncol[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) {
@@ -770,6 +781,12 @@ void srbd_admm_kernel(const SrbdArgs a) {
   row_scans<W>(S, N, false);
   bsync<W>();
   float qv = valid ? bqp_t<W>(S, step, comp, lo, hi, dtm, dt2m) : 0.0f;
+  const float q_raw = qv;  // unscaled gradient entry (persistent record)
+  // OSQP's update path runs scale_data on the new P with the PREVIOUS q in
+  // place (osqp_update_P precedes osqp_update_lin_cost): the cost scale's
+  // ||q|| comes from the previous call's gradient, scaled alongside
+  float qsv = qv;
+  if (p_same) qsv = valid ? prec[84 * N + 12 * step + 3 * leg + comp] : 0.0f;
 
   QL_PHASE(2);
   // ---------------- 5. constraint rows owned by this lane (ConvexMpc.cpp:47-59, :227-249)
@@ -787,7 +804,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
   S.pair[t] = 4 * step + leg;
 
   Row<W> K;
-  float cinv = 1.0f, rho = fminf(fmaxf(a.rho, 1e-6f), 1e6f), rvi = 1.0f / rho;
+  float cinv = 1.0f, rho = fminf(fmaxf(p_same ? prec[NP] : a.rho, 1e-6f), 1e6f), rvi = 1.0f / rho;
   bool eq0 = false;
   float qn[2] = {0.0f, 0.0f};
 #define RV0 (eq0 ? 1e3f * rho : rho)
@@ -913,6 +930,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
         rE0 *= Et0;
         rE1 *= Et1;
         qv *= Dt;
+        qsv *= Dt;
         Dr *= Dt;
         const int buf = it & 1;
         reinterpret_cast<float *>(&S.bc[buf][0])[t] = Dr;
@@ -935,12 +953,13 @@ void srbd_admm_kernel(const SrbdArgs a) {
         const float cn2 = Dr * fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
         // cost scaling: mean column norm of P (= row norm, P symmetric) vs ||q||_inf
         const float sumP = bsum<W>(valid ? cn2 : 0.0f, S.red);
-        float qm[1] = {valid ? fabsf(qv) : 0.0f};
+        float qm[1] = {valid ? fabsf(qsv) : 0.0f};
         bmax<W, 1>(qm, S.red);
         const float meanP = cs * sumP * inv_n;
         // v_rcp_f32 (1 ulp), like the rsq above: a heuristic factor
         const float ctc = __builtin_amdgcn_rcpf(limit_scaling(fmaxf(meanP, limit_scaling(qm[0]))));
         qv *= ctc;
+        qsv *= ctc;
         cs *= ctc;
         cnP = cn2 * cs;
       }
@@ -995,12 +1014,23 @@ void srbd_admm_kernel(const SrbdArgs a) {
     }
     if (first) {
       first = false;
-      if (a.warm_start) {
-        const int nu = 12 * N, ncn = 20 * N;
-        const float *wx = a.warm + b * (nu + ncn);
-        const float *wy = wx + nu;
-        x = valid ? wx[12 * step + 3 * leg + comp] / Dr : 0.0f;
-        const int rbase = 20 * step + 5 * leg + 2 * comp;
+      const int vidx = 12 * step + 3 * leg + comp, rbase = 20 * step + 5 * leg + 2 * comp;
+      if (p_same) {
+        // live workspace (osqp_solve without cold start): the scaled
+        // iterates of the last call as they are
+        x = valid ? prec[vidx] : 0.0f;
+        z.x = valid ? prec[12 * N + rbase] : 0.0f;
+        z.y = (valid && xy) ? prec[12 * N + rbase + 1] : 0.0f;
+        y.x = valid ? prec[32 * N + rbase] : 0.0f;
+        y.y = (valid && xy) ? prec[32 * N + rbase + 1] : 0.0f;
+      } else if (a.warm_start == 1 || p_init) {
+        // osqp_warm_start from the unscaled x | y: the caller's buffer
+        // (warm_start 1) or, for a persistent solver whose stance set
+        // changed, the record's last solution (OsqpEigen re-initialisation
+        // + setPrimal/DualVariable)
+        const float *wx = a.warm_start == 1 ? a.warm + b * (32 * N) : prec + 52 * N;
+        const float *wy = wx + 12 * N;
+        x = valid ? wx[vidx] / Dr : 0.0f;
         y.x = valid ? wy[rbase] / rE0 * cs : 0.0f;
         y.y = (valid && xy) ? wy[rbase + 1] / rE1 * cs : 0.0f;
         const float n1 = lane_next(x), n2 = lane_next(n1);
@@ -1207,7 +1237,30 @@ void srbd_admm_kernel(const SrbdArgs a) {
       o = cp == 0 ? (R00 * f0 + R10 * f1) : (cp == 1 ? (R01 * f0 + R11 * f1) : f2);
     a.u0[b * 12 + t] = bad ? NAN : o;
   }
-  if (a.warm_start) {
+  if (prec) {  // the persistent record for the next call
+    for (int k = t; k < NP + 4; k += NC) prec[k] = 0.0f;
+    __syncthreads();
+    if (valid) {
+      const int vidx = 12 * step_o + 3 * leg_o + comp, rbase = 20 * step_o + 5 * leg_o + 2 * comp;
+      prec[vidx] = x;
+      prec[52 * N + vidx] = xu;
+      prec[84 * N + vidx] = q_raw;
+      prec[12 * N + rbase] = z.x;
+      prec[32 * N + rbase] = y.x;
+      prec[64 * N + rbase] = cinv * S.aux[1][t] * y.x;
+      if (xy) {
+        prec[12 * N + rbase + 1] = z.y;
+        prec[32 * N + rbase + 1] = y.y;
+        prec[64 * N + rbase + 1] = cinv * S.aux[2][t] * y.y;
+      }
+    }
+    for (int k = t; k < 4 * N; k += NC) prec[96 * N + k] = S.ct[k] ? 1.0f : 0.0f;
+    if (t == 0) {
+      prec[NP] = rho;
+      prec[NP + 1] = 1.0f;
+    }
+  }
+  if (a.warm_start == 1) {
     const int nu = 12 * N, ncn = 20 * N;
     float *wx = a.warm + b * (nu + ncn);
     float *wy = wx + nu;
@@ -1288,6 +1341,7 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   if (spec->horizon < 1 || spec->horizon > kMaxN) return QLOCO_BAD_SIZE;
   if (batch == 0) return QLOCO_OK;
   if (!x0 || !x_ref || !feet || !contacts || !u0) return QLOCO_ERR_ARG;
+  if (spec->warm_start < 0 || spec->warm_start > 2) return QLOCO_ERR_ARG;
   if (spec->warm_start && !warm) return QLOCO_ERR_ARG;
   if (spec->mass <= 0.0f || spec->dt <= 0.0f) return QLOCO_ERR_ARG;
   // OSQP polishing (off in OSQP's defaults and in the reference, which never

@@ -366,8 +366,12 @@ int PRMPCClass::Indexfind(double goal_P) {
 // ---------------------------------------------------------------- ConvexMpcBatch
 ConvexMpcBatch::ConvexMpcBatch(int batch, const qloco_srbd_spec *sp) : batch_(batch) {
   if (batch < 1) throw Error("ConvexMpcBatch: batch < 1", QLOCO_ERR_ARG);
-  if (sp) spec = *sp;
-  else qloco_srbd_spec_default(&spec);
+  if (sp) {
+    spec = *sp;
+  } else {
+    qloco_srbd_spec_default(&spec);
+    spec.warm_start = 2;       // the reference's persistent member solver
+  }
   spec.feet_per_step = 0;      // compute_grf passes one foot_pos_abs (:527-531)
   spec.contacts_per_step = 0;  // and one contacts[4] (ConvexMpc.cpp:232-249)
   spec.output_frame = 1;       // root_rot_mat' u (:596-599)
@@ -379,8 +383,20 @@ ConvexMpcBatch::ConvexMpcBatch(int batch, const qloco_srbd_spec *sp) : batch_(ba
   d_u0_ = dalloc<float>(arena_, B * 12);
   d_st_ = dalloc<int32_t>(arena_, B);
   d_it_ = dalloc<int32_t>(arena_, B);
+  if (spec.warm_start == 2) {  // per-robot persistent solver record
+    d_rec_ = dalloc<float>(arena_, B * QLOCO_SRBD_PERSIST_LEN(N));
+    reset();
+  }
   status.assign(B, 0);
   iters.assign(B, 0);
+}
+
+void ConvexMpcBatch::reset() {
+  if (!d_rec_) return;
+  hip_ok(hipMemsetAsync(d_rec_, 0,
+                        sizeof(float) * (size_t)batch_ * QLOCO_SRBD_PERSIST_LEN(spec.horizon),
+                        (hipStream_t)arena_.stream()),
+         "hipMemsetAsync");
 }
 
 void ConvexMpcBatch::solve_device(const float *x0, const float *x_ref, const float *feet,
@@ -388,7 +404,7 @@ void ConvexMpcBatch::solve_device(const float *x0, const float *x_ref, const flo
   int32_t legs = 0;  // constant contacts over the horizon: max stance legs = 4N worst case
   legs = 4 * spec.horizon;
   abi_ok(qloco_srbd_solve_ex(&spec, batch_, x0, x_ref, feet, contacts, u0, nullptr, st, it,
-                             nullptr, nullptr, nullptr, legs, arena_.stream()),
+                             nullptr, nullptr, d_rec_, legs, arena_.stream()),
          "qloco_srbd_solve_ex");
 }
 
@@ -445,7 +461,7 @@ void ConvexMpcBatch::compute_grf(const A1MpcState *s, double *forces) {
   arena_.upload(d_feet_, feet.data(), sizeof(float) * B * 12);
   arena_.upload(d_ct_, ct.data(), B * 4);
   abi_ok(qloco_srbd_solve_ex(&spec, batch_, d_x0_, d_xr_, d_feet_, d_ct_, d_u0_, nullptr, d_st_,
-                             d_it_, nullptr, nullptr, nullptr, maxlegs, arena_.stream()),
+                             d_it_, nullptr, nullptr, d_rec_, maxlegs, arena_.stream()),
          "qloco_srbd_solve_ex");
   std::vector<float> u0(B * 12);
   arena_.download(u0.data(), d_u0_, sizeof(float) * B * 12);
@@ -458,6 +474,51 @@ void ConvexMpcBatch::compute_grf(const A1MpcState *s, double *forces) {
       if (std::isnan(f[0]) || std::isnan(f[1]) || std::isnan(f[2])) continue;  // :597 guard
       for (int c = 0; c < 3; ++c) forces[b * 12 + 3 * l + c] = f[c];
     }
+}
+
+
+// ---------------------------------------------------------------- A1QpBatch
+A1QpBatch::A1QpBatch(int batch, const qloco_a1_params *p) : batch_(batch) {
+  if (batch < 1) throw Error("A1QpBatch: batch < 1", QLOCO_ERR_ARG);
+  if (p) params = *p;
+  else qloco_a1_params_default(&params);
+  const size_t B = batch;
+  d_state_ = dalloc<double>(arena_, B * QLOCO_A1_STATE_LEN);
+  d_forces_ = dalloc<double>(arena_, B * 12);
+  d_ct_ = dalloc<uint8_t>(arena_, B * 4);
+  d_st_ = dalloc<int32_t>(arena_, B);
+  d_it_ = dalloc<int32_t>(arena_, B);
+  status.assign(B, 0);
+  iters.assign(B, 0);
+}
+
+void A1QpBatch::compute_grf(const A1QpState *s, double *forces) {
+  const size_t B = batch_;
+  std::vector<double> st(B * QLOCO_A1_STATE_LEN);
+  std::vector<uint8_t> ct(B * 4);
+  for (size_t b = 0; b < B; ++b) {  // the record layout of include/qloco.h section 9
+    double *r = &st[b * QLOCO_A1_STATE_LEN];
+    const double *src[8] = {s[b].root_pos,     s[b].root_pos_d,     s[b].root_euler,
+                            s[b].root_euler_d, s[b].root_lin_vel,   s[b].root_lin_vel_d,
+                            s[b].root_ang_vel, s[b].root_ang_vel_d};
+    for (int f = 0; f < 8; ++f)
+      for (int k = 0; k < 3; ++k) r[3 * f + k] = src[f][k];
+    for (int k = 0; k < 9; ++k) {
+      r[24 + k] = s[b].root_rot_mat[k];
+      r[33 + k] = s[b].root_rot_mat_z[k];
+    }
+    for (int k = 0; k < 12; ++k) r[42 + k] = s[b].foot_pos_abs[k];
+    for (int l = 0; l < 4; ++l) ct[b * 4 + l] = s[b].contacts[l] ? 1 : 0;
+  }
+  arena_.upload(d_state_, st.data(), sizeof(double) * st.size());
+  arena_.upload(d_ct_, ct.data(), ct.size());
+  abi_ok(qloco_a1_qp_solve(&params, batch_, d_state_, d_ct_, d_forces_, nullptr, d_st_, d_it_,
+                           nullptr, nullptr, arena_.stream()),
+         "qloco_a1_qp_solve");
+  arena_.download(forces, d_forces_, sizeof(double) * B * 12);
+  arena_.download(status.data(), d_st_, sizeof(int32_t) * B);
+  arena_.download(iters.data(), d_it_, sizeof(int32_t) * B);
+  arena_.sync();
 }
 
 

@@ -154,3 +154,38 @@ class BatchedConvexMpc:
             ptr(out.get("H")), ptr(out.get("g")), ptr(out.get("lb")), ptr(out.get("ub")),
             ptr(out.get("Aqp")), ptr(out.get("Bqp")), C.c_void_p(stream)), "qloco_srbd_build")
         return out
+
+
+def persist_len(horizon):
+    """Floats per instance of the persistent-solver record
+    (QLOCO_SRBD_PERSIST_LEN, include/qloco.h)."""
+    return 100 * int(horizon) + 4
+
+
+class PersistentConvexMpc(BatchedConvexMpc):
+    """B controllers, each with the reference's member OSQP solver
+    (A1RobotControl.h:67) kept across control ticks: the first solve sets it
+    up, later ones take OSQP's update path -- new P / q / bounds into the
+    live workspace, Ruiz recomputed with the previous gradient in the cost
+    scale, the adapted rho and the scaled iterates carried over
+    (A1RobotControl.cpp:556-578).  A controller whose stance set changes is
+    re-initialised and warm-started from its last solution.  The per-instance
+    record lives on the device (`record`, zeroed by reset())."""
+
+    def __init__(self, batch, device, spec=None, **overrides):
+        import torch
+        super().__init__(spec, **overrides)
+        self.spec.warm_start = 2
+        self.batch = int(batch)
+        self.record = torch.zeros((self.batch, persist_len(self.spec.horizon)),
+                                  dtype=torch.float32, device=device)
+
+    def reset(self):
+        self.record.zero_()
+
+    def solve(self, x0, x_ref, feet, contacts, out=None, full=False, max_legs=None,
+              stream=None):
+        if x0.shape[0] != self.batch:
+            raise ValueError("batch %d, record holds %d controllers" % (x0.shape[0], self.batch))
+        return super().solve(x0, x_ref, feet, contacts, out=out, full=full, max_legs=max_legs,
+                             warm=self.record, stream=stream)

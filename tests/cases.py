@@ -23,3 +23,30 @@ def force_inputs(rng, B):
     return dict(com_des=base, leg_des=feet.reshape(B, 12), F_force_des=F_sum,
                 rfoot_des=rfoot, lfoot_des=lfoot, base_p=base, feet_p=feet.reshape(B, 12),
                 FT_total_des=F_sum, mode=mode, right_support=rs, y_coef=y)
+
+
+def closed_loop_srbd(N, B, ticks, seed=20261015, switch_at=None):
+    """A control-loop sequence of SRBD MPC inputs (float32, per tick): the
+    synthetic trot instances drift as the robot would between 2.5 ms MPC
+    ticks (position by v dt, attitude by omega dt, the reference trajectory
+    moving with them), and from tick `switch_at` on the even controllers
+    switch trot phase (their stance set changes, the persistent solver's
+    re-initialisation path).  Returns a list of (x0, x_ref, feet, contacts)."""
+    from quadrupedal_loco_amd import srbd
+    x0, xr, ft, ct = srbd.generate(seed, N, B, "trot")
+    dt = 0.0025
+    seq = []
+    for t in range(ticks):
+        x = x0.astype(np.float64).copy()
+        r = xr.astype(np.float64).reshape(B, N, 13).copy()
+        dp = dt * t * x[:, 9:12]
+        da = 0.5 * dt * t * x[:, 6:9]
+        x[:, 3:6] += dp
+        x[:, 0:3] += da
+        r[:, :, 3:5] += dp[:, None, :2]
+        r[:, :, 2] += da[:, None, 2]
+        c = ct.copy()
+        if switch_at is not None and t >= switch_at:
+            c[0::2] = 1 - c[0::2]
+        seq.append((x.astype(np.float32), r.reshape(B, 13 * N).astype(np.float32), ft.copy(), c))
+    return seq

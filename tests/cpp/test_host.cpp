@@ -216,6 +216,107 @@ static void test_convex_mpc() {
               mpc.iters[0]);
 }
 
+// The reference's member solver semantics: a default-constructed
+// ConvexMpcBatch keeps each robot's OSQP solver across compute_grf calls
+// (A1RobotControl.cpp:556-578); an identical second call resumes at the
+// converged iterate and stops at the first termination check, reset()
+// restores the cold solve.
+static void test_convex_mpc_persistent() {
+  qloco::ConvexMpcBatch mpc(2);
+  CHECK(mpc.spec.warm_start == 2, "default ConvexMpcBatch is persistent");
+  qloco::A1MpcState st[2] = {};
+  for (auto &s : st) {
+    s.root_pos[2] = 0.30;
+    s.root_pos_d[2] = 0.30;
+    s.root_euler[2] = 0.4;
+    s.root_lin_vel[0] = 0.2;
+    const double c = std::cos(0.4), sn = std::sin(0.4);
+    const double R[9] = {c, sn, 0, -sn, c, 0, 0, 0, 1};
+    for (int k = 0; k < 9; ++k) s.root_rot_mat[k] = R[k];
+    const double feet[12] = {0.15, 0.127, -0.31, 0.15, -0.127, -0.31,
+                             -0.225, 0.127, -0.31, -0.225, -0.127, -0.31};
+    for (int k = 0; k < 12; ++k) s.foot_pos_abs[k] = feet[k];
+    s.contacts[0] = s.contacts[3] = true;
+  }
+  st[1].contacts[0] = st[1].contacts[3] = false;
+  st[1].contacts[1] = st[1].contacts[2] = true;
+  double f1[24] = {0}, f2[24] = {0}, f3[24] = {0};
+  mpc.compute_grf(st, f1);
+  const int cold = mpc.iters[0];
+  mpc.compute_grf(st, f2);
+  for (int b = 0; b < 2; ++b) {
+    CHECK(mpc.status[b] == QLOCO_OK, "persistent status %d", mpc.status[b]);
+    CHECK(mpc.iters[b] == 25, "resumed solve iters %d (cold %d)", mpc.iters[b], cold);
+  }
+  mpc.reset();
+  mpc.compute_grf(st, f3);
+  CHECK(mpc.iters[0] == cold, "after reset: cold again (%d vs %d)", mpc.iters[0], cold);
+  for (int k = 0; k < 24; ++k) CHECK(f3[k] == f1[k], "reset reproduces the cold solve [%d]", k);
+  std::printf("persistent compute_grf ok: cold %d iters, resumed %d\n", cold, mpc.iters[1]);
+}
+
+// A1RobotControl::compute_grf QP branch (A1QpBatch) vs oracle/a1_qp.c.
+static void test_a1_qp() {
+  const int B = 8;
+  qloco::A1QpBatch qp(B);
+  std::vector<qloco::A1QpState> st(B);
+  std::mt19937_64 rng(7);
+  std::uniform_real_distribution<double> U(-1.0, 1.0);
+  qo_a1_params prm;
+  qo_a1_params_default(&prm);
+  qo_admm_settings set;
+  qo_admm_settings_default(&set);
+  for (int b = 0; b < B; ++b) {
+    qloco::A1QpState &s = st[b];
+    s = qloco::A1QpState{};
+    const double yaw = 3.0 * U(rng);
+    const double c = std::cos(yaw), sn = std::sin(yaw);
+    const double R[9] = {c, sn, 0, -sn, c, 0, 0, 0, 1};
+    for (int k = 0; k < 9; ++k) s.root_rot_mat[k] = s.root_rot_mat_z[k] = R[k];
+    s.root_euler[2] = yaw;
+    s.root_euler_d[2] = yaw + 0.2 * U(rng);
+    for (int k = 0; k < 3; ++k) {
+      s.root_lin_vel[k] = 0.3 * U(rng);
+      s.root_ang_vel[k] = 0.3 * U(rng);
+    }
+    s.root_pos[2] = 0.28;
+    s.root_pos_d[2] = 0.30;
+    const double fb[12] = {0.17, 0.15, -0.3, 0.17, -0.15, -0.3, -0.17, 0.15, -0.3, -0.17, -0.15, -0.3};
+    for (int l = 0; l < 4; ++l)  // foot_pos_abs = R * foot_pos_rel
+      for (int r = 0; r < 3; ++r)
+        s.foot_pos_abs[3 * l + r] =
+            R[r] * fb[3 * l] + R[3 + r] * fb[3 * l + 1] + R[6 + r] * fb[3 * l + 2];
+    for (int l = 0; l < 4; ++l) s.contacts[l] = (b & 1) ? (l == 1 || l == 2) : (l == 0 || l == 3);
+    if (b == 5) s.contacts[0] = s.contacts[1] = s.contacts[2] = s.contacts[3] = true;
+  }
+  std::vector<double> f(B * 12);
+  qp.compute_grf(st.data(), f.data());
+  for (int b = 0; b < B; ++b) {
+    const qloco::A1QpState &s = st[b];
+    double rec[QO_A1_STATE_LEN];
+    const double *src[8] = {s.root_pos, s.root_pos_d, s.root_euler, s.root_euler_d,
+                            s.root_lin_vel, s.root_lin_vel_d, s.root_ang_vel, s.root_ang_vel_d};
+    for (int q = 0; q < 8; ++q)
+      for (int k = 0; k < 3; ++k) rec[3 * q + k] = src[q][k];
+    for (int k = 0; k < 9; ++k) {
+      rec[24 + k] = s.root_rot_mat[k];
+      rec[33 + k] = s.root_rot_mat_z[k];
+    }
+    for (int k = 0; k < 12; ++k) rec[42 + k] = s.foot_pos_abs[k];
+    uint8_t ct[4];
+    for (int l = 0; l < 4; ++l) ct[l] = s.contacts[l];
+    double fo[12];
+    qo_admm_info info;
+    qo_a1_compute_grf(&prm, &set, rec, ct, fo, nullptr, &info);
+    CHECK(qp.status[b] == info.status && qp.iters[b] == info.iters, "A1 QP robot %d status/iters",
+          b);
+    for (int k = 0; k < 12; ++k)
+      CHECK(std::fabs(f[b * 12 + k] - fo[k]) < 1e-5, "A1 QP robot %d [%d] %.9f vs %.9f", b, k,
+            f[b * 12 + k], fo[k]);
+  }
+  std::printf("A1 QP compute_grf ok\n");
+}
+
 // Kinematicclass: per-leg calls (servo.cpp:734-741 / :1038-1051 pattern)
 // and a batch, against the C restatement (oracle/kinematics.c).
 static void test_kinematics() {
@@ -381,6 +482,8 @@ int main() {
     test_qpsolver();
     test_body_mpc();
     test_convex_mpc();
+    test_convex_mpc_persistent();
+    test_a1_qp();
     test_kinematics();
     test_rt_node();
     test_servo_block();

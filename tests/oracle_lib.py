@@ -155,6 +155,10 @@ def lib():
         L.qo_rt_tick_n.argtypes = [C.c_void_p, C.c_int64] + [C.c_void_p] * 6
         L.qo_inv4.argtypes = [dp, dp]
         L.qo_support_phase.argtypes = [C.c_int64] + [C.c_void_p] * 7
+        L.qo_srbd_persist_step.restype = C.c_int
+        L.qo_srbd_persist_step.argtypes = [dp, C.POINTER(SrbdSpec), C.POINTER(AdmmSettings),
+                                           fp, fp, fp, C.c_int, u8p, C.c_int, dp,
+                                           C.POINTER(AdmmInfo)]
         L.qo_a1_params_default.argtypes = [C.POINTER(A1Params)]
         L.qo_a1_qp_build.argtypes = [C.POINTER(A1Params), dp, u8p, dp, dp, dp, dp, dp, dp]
         L.qo_a1_compute_grf.restype = C.c_int
@@ -434,3 +438,33 @@ def a1_compute_grf(state, contacts, params=None, **admm):
     lib().qo_a1_compute_grf(C.byref(p), C.byref(st), P(s), P(c, C.c_uint8), P(f), P(x),
                             C.byref(info))
     return f, x, info
+
+
+# ---- persistent SRBD solver (oracle/persist.c)
+def persist_len(N):
+    return 100 * N + 4
+
+
+class PersistentMpc:
+    """The reference's member OSQP solver restated on the stance-only QP,
+    one record per controller."""
+
+    def __init__(self, N, **admm):
+        self.N = N
+        self.sp = srbd_spec(N=N)
+        self.st = admm_settings(**admm)
+        self.rec = np.zeros(persist_len(N))
+
+    def step(self, x0, xr, ft, ct):
+        u = np.zeros(12 * self.N)
+        info = AdmmInfo()
+        x0 = np.ascontiguousarray(x0, np.float32)
+        xr = np.ascontiguousarray(xr, np.float32)
+        ft = np.ascontiguousarray(ft, np.float32)
+        ct = np.ascontiguousarray(ct, np.uint8)
+        fps = int(ft.size == 12 * self.N and self.N > 1)
+        cps = int(ct.size == 4 * self.N and self.N > 1)
+        lib().qo_srbd_persist_step(P(self.rec), C.byref(self.sp), C.byref(self.st),
+                                   P(x0, C.c_float), P(xr, C.c_float), P(ft, C.c_float), fps,
+                                   P(ct, C.c_uint8), cps, P(u), C.byref(info))
+        return u, info
