@@ -601,7 +601,9 @@ __device__ unsigned int g_phase[1 << 20];
 #endif
 constexpr int64_t kSmallBatch = QLOCO_SMALL_BATCH;
 
-template <int W, int WPE>
+// WS: a warm-start mode (1 or 2) may be set.  The cold-start instantiation
+// (the headline path) carries none of the warm / persistent-record code.
+template <int W, int WPE, bool WS>
 __global__ __launch_bounds__(64 * W)
 __attribute__((amdgpu_waves_per_eu(WPE))) QLOCO_SRBD_NUM_VGPR_ATTR
 void srbd_admm_kernel(const SrbdArgs a) {
@@ -664,7 +666,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
   // persistent solver (warm_start == 2, A1RobotControl.cpp:556-578): the
   // record of this instance's last call (layout: QLOCO_SRBD_PERSIST_LEN)
   const int NP = 100 * N;
-  float *prec = a.warm_start == 2 ? a.warm + b * (int64_t)(NP + 4) : nullptr;
+  float *prec = (WS && a.warm_start == 2) ? a.warm + b * (int64_t)(NP + 4) : nullptr;
   bool p_init = false, p_same = false;
   if (prec) {
     p_init = prec[NP + 1] > 0.5f;
@@ -1023,7 +1025,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
         z.y = (valid && xy) ? prec[12 * N + rbase + 1] : 0.0f;
         y.x = valid ? prec[32 * N + rbase] : 0.0f;
         y.y = (valid && xy) ? prec[32 * N + rbase + 1] : 0.0f;
-      } else if (a.warm_start == 1 || p_init) {
+      } else if (WS && (a.warm_start == 1 || p_init)) {
         // osqp_warm_start from the unscaled x | y: the caller's buffer
         // (warm_start 1) or, for a persistent solver whose stance set
         // changed, the record's last solution (OsqpEigen re-initialisation
@@ -1260,7 +1262,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
       prec[NP + 1] = 1.0f;
     }
   }
-  if (a.warm_start == 1) {
+  if (WS && a.warm_start == 1) {
     const int nu = 12 * N, ncn = 20 * N;
     float *wx = a.warm + b * (nu + ncn);
     float *wy = wx + nu;
@@ -1396,12 +1398,21 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   hipStream_t st = (hipStream_t)stream;
   a.leg_lo = 0;
   a.leg_hi = 1 << 30;
+  const bool ws = spec->warm_start != 0;
   auto launch_w1 = [&]() {
-    if (batch <= kSmallBatch)
-      hipLaunchKernelGGL((srbd_admm_kernel<1, 2>), dim3((unsigned)batch), dim3(64), 0, st, a);
-    else
-      hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU>), dim3((unsigned)batch),
-                         dim3(64), 0, st, a);
+    if (batch <= kSmallBatch) {
+      if (ws)
+        hipLaunchKernelGGL((srbd_admm_kernel<1, 2, true>), dim3((unsigned)batch), dim3(64), 0, st, a);
+      else
+        hipLaunchKernelGGL((srbd_admm_kernel<1, 2, false>), dim3((unsigned)batch), dim3(64), 0, st, a);
+    } else {
+      if (ws)
+        hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, true>),
+                           dim3((unsigned)batch), dim3(64), 0, st, a);
+      else
+        hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, false>),
+                           dim3((unsigned)batch), dim3(64), 0, st, a);
+    }
   };
   if (legs <= kLegsPerWave) {
     launch_w1();
@@ -1411,8 +1422,12 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
     QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel<1> launch");
     a.leg_lo = kLegsPerWave + 1;
     a.leg_hi = 1 << 30;
-    hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2>), dim3((unsigned)batch),
-                       dim3(128), 0, st, a);
+    if (ws)
+      hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, true>),
+                         dim3((unsigned)batch), dim3(128), 0, st, a);
+    else
+      hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, false>),
+                         dim3((unsigned)batch), dim3(128), 0, st, a);
   }
   QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel launch");
   return QLOCO_OK;
