@@ -364,8 +364,15 @@ int PRMPCClass::Indexfind(double goal_P) {
 }
 
 // ---------------------------------------------------------------- ConvexMpcBatch
-ConvexMpcBatch::ConvexMpcBatch(int batch, const qloco_srbd_spec *sp) : batch_(batch) {
-  if (batch < 1) throw Error("ConvexMpcBatch: batch < 1", QLOCO_ERR_ARG);
+// argument check in the member-initialiser list: batch_ is declared before
+// the DeviceArena, so a bad batch is refused before any device call
+static int positive_batch(int batch, const char *who) {
+  if (batch < 1) throw Error(std::string(who) + ": batch < 1", QLOCO_ERR_ARG);
+  return batch;
+}
+
+ConvexMpcBatch::ConvexMpcBatch(int batch, const qloco_srbd_spec *sp)
+    : batch_(positive_batch(batch, "ConvexMpcBatch")) {
   if (sp) {
     spec = *sp;
   } else {
@@ -478,8 +485,8 @@ void ConvexMpcBatch::compute_grf(const A1MpcState *s, double *forces) {
 
 
 // ---------------------------------------------------------------- A1QpBatch
-A1QpBatch::A1QpBatch(int batch, const qloco_a1_params *p) : batch_(batch) {
-  if (batch < 1) throw Error("A1QpBatch: batch < 1", QLOCO_ERR_ARG);
+A1QpBatch::A1QpBatch(int batch, const qloco_a1_params *p)
+    : batch_(positive_batch(batch, "A1QpBatch")) {
   if (p) params = *p;
   else qloco_a1_params_default(&params);
   const size_t B = batch;

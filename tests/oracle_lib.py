@@ -12,6 +12,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "_build", "libqloco_oracle.so")
+if os.environ.get("QLOCO_ORACLE_UBSAN") == "1":  # tests/test_sanitizers.py
+    LIB_PATH = os.path.join(ORACLE_DIR, "_build_ubsan", "libqloco_oracle.so")
 
 _lib = None
 
@@ -22,7 +24,8 @@ u8p = C.POINTER(C.c_uint8)
 
 
 def build():
-    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR] +
+                   (["asan"] if "_build_ubsan" in LIB_PATH else []), check=True)
 
 
 class SrbdSpec(C.Structure):
