@@ -102,7 +102,7 @@ typedef struct qloco_srbd_spec {
 /* Go1 SRBD constants + OSQP default settings. */
 void qloco_srbd_spec_default(qloco_srbd_spec *spec);
 
-/* Largest horizon / stance-variable count the compiled kernels accept. */
+/* Largest stance-variable count the compiled kernels accept (3 x 4 x 20). */
 int qloco_srbd_max_stance_vars(void);
 
 /* Batched build + ADMM solve (the hot path).  Device pointers:
@@ -123,11 +123,13 @@ int qloco_srbd_solve(const qloco_srbd_spec *spec, int64_t batch, const float *x0
 /* Extended form of qloco_srbd_solve: additionally returns rho_updates[B]
  * (number of adaptive-rho refactorisations) and takes max_stance_legs, the
  * largest number of stance (step, leg) pairs of any instance in the batch,
- * or 0 = unknown (assume 4N).  <= 21: one launch of the one-wavefront
- * kernel; otherwise two launches on the stream, instances with <= 21 stance
- * pairs in one-wavefront and the others in two-wavefront workgroups.  An
- * instance with more than 42 stance pairs gets status QLOCO_BAD_SIZE and NaN
- * forces. */
+ * or 0 = unknown (assume 4N).  Instances run by class: <= 21 stance pairs
+ * in one-wavefront workgroups, 22..42 in two-wavefront workgroups, 43..80
+ * (up to N = 20 all-stance, 240 variables) in the wide 512-thread kernel --
+ * one launch per class the maximum admits, on the stream.  Any N <= 20
+ * schedule is accepted; an instance with more stance pairs than a
+ * caller-supplied max_stance_legs admits gets status QLOCO_BAD_SIZE, NaN u0 /
+ * u / obj and iters = 0. */
 int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, const float *x0,
                         const float *x_ref, const float *feet, const uint8_t *contacts,
                         float *u0, float *u, int32_t *status, int32_t *iters,

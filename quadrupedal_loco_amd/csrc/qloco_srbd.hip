@@ -658,9 +658,16 @@ void srbd_admm_kernel(const SrbdArgs a) {
   const int nlegs = uni(S.nlegs);
   const int n = 3 * nlegs;
   if (nlegs < a.leg_lo || nlegs > a.leg_hi) return;  // the other launch's instance
-  if (nlegs > kLegsPerWave * W) {  // uniform: host picks W from the batch max
+  if (nlegs > kLegsPerWave * W) {  // uniform: the caller's max_stance_legs was too small
     if (t < 12) a.u0[b * 12 + t] = NAN;
-    if (t == 0 && a.status) a.status[b] = QLOCO_BAD_SIZE;
+    if (a.u)
+      for (int k = t; k < 12 * N; k += NC) a.u[b * 12 * N + k] = NAN;
+    if (t == 0) {
+      if (a.status) a.status[b] = QLOCO_BAD_SIZE;
+      if (a.iters) a.iters[b] = 0;
+      if (a.rho_updates) a.rho_updates[b] = 0;
+      if (a.obj) a.obj[b] = NAN;
+    }
     return;
   }
   // persistent solver (warm_start == 2, A1RobotControl.cpp:556-578): the
@@ -1286,6 +1293,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
 
 }  // namespace qloco
 
+#include "qloco_srbd_big.inc"
+
 using namespace qloco;
 
 extern "C" void qloco_srbd_spec_default(qloco_srbd_spec *s) {
@@ -1331,7 +1340,7 @@ extern "C" int qloco_phase_read(unsigned int *host, size_t count) {
 }
 #endif
 
-extern "C" int qloco_srbd_max_stance_vars(void) { return 3 * kLegsPerWave * 2; }
+extern "C" int qloco_srbd_max_stance_vars(void) { return 3 * kBigLegs; }
 
 extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, const float *x0,
                                    const float *x_ref, const float *feet,
@@ -1388,12 +1397,13 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   a.status = status;
   a.iters = iters;
   a.rho_updates = rho_updates;
-  // W per instance: instances with <= 21 stance legs run one-wave workgroups,
-  // larger ones two-wave workgroups.  When the batch may hold both (the
-  // caller's maximum, or 4N when unknown, exceeds 21) the batch goes through
-  // two launches on the stream, each skipping the other's instances after
-  // counting its stance legs; instances above 42 legs get QLOCO_BAD_SIZE in
-  // the second.
+  // Kernel per instance: <= 21 stance legs one-wave workgroups, 22..42
+  // two-wave workgroups, 43..80 the wide kernel (qloco_srbd_big.inc).  When
+  // the batch may hold several classes (the caller's maximum, or 4N when
+  // unknown, says so) it goes through one launch per class on the stream,
+  // each skipping the others' instances after counting its stance legs.  The
+  // last launch takes every instance above the previous classes, so an
+  // instance beyond a too-small caller maximum gets QLOCO_BAD_SIZE there.
   const int legs = max_stance_legs > 0 ? max_stance_legs : 4 * spec->horizon;
   hipStream_t st = (hipStream_t)stream;
   a.leg_lo = 0;
@@ -1421,13 +1431,24 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
     launch_w1();
     QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel<1> launch");
     a.leg_lo = kLegsPerWave + 1;
-    a.leg_hi = 1 << 30;
+    a.leg_hi = legs <= 2 * kLegsPerWave ? (1 << 30) : 2 * kLegsPerWave;
     if (ws)
       hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, true>),
                          dim3((unsigned)batch), dim3(128), 0, st, a);
     else
       hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, false>),
                          dim3((unsigned)batch), dim3(128), 0, st, a);
+    if (legs > 2 * kLegsPerWave) {
+      QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel<2> launch");
+      a.leg_lo = 2 * kLegsPerWave + 1;
+      a.leg_hi = 1 << 30;  // <= 4N = kBigLegs by construction
+      if (ws)
+        hipLaunchKernelGGL((srbd_admm_big_kernel<true>), dim3((unsigned)batch), dim3(kBigThreads),
+                           0, st, a);
+      else
+        hipLaunchKernelGGL((srbd_admm_big_kernel<false>), dim3((unsigned)batch), dim3(kBigThreads),
+                           0, st, a);
+    }
   }
   QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel launch");
   return QLOCO_OK;

@@ -58,7 +58,8 @@ def test_srbd_spec_defaults_are_reference_constants():
     assert s.max_iter == 4000 and s.check_termination == 25 and s.scaling == 10
     assert s.adaptive_rho == 1 and s.adaptive_rho_interval == 0
     assert s.adaptive_rho_tolerance == 5.0 and s.warm_start == 0 and s.polish == 0
-    assert _lib.lib().qloco_srbd_max_stance_vars() == 126
+    # up to N = 20 all-stance: 80 stance legs, 240 variables (the wide kernel)
+    assert _lib.lib().qloco_srbd_max_stance_vars() == 240
 
 
 def test_force_params_defaults():
