@@ -174,6 +174,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every usable host core)")
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--shard", choices=("auto", "contiguous", "interleaved"), default="auto",
+                    help="instance ids per rank: contiguous ranges, or stride-interleaved "
+                         "(SURVEY.md 8e; auto: interleaved for the mixed-schedule config 5)")
     ap.add_argument("--overlap", action="store_true",
                     help="N > 1: run each step's all-gather under the next solve (double-"
                          "buffered u0); off by default: on one GPU the RCCL kernel sharing "
@@ -219,9 +222,14 @@ def main():
     from quadrupedal_loco_amd import srbd
 
     B, N = args.batch, args.horizon
-    from quadrupedal_loco_amd.dist import shard_range
-    first, _ = shard_range(B, rank)
-    x0, xr, ft, ct = srbd.generate(SEED, N, B, args.gait, first=first)
+    from quadrupedal_loco_amd.dist import interleaved_shard, shard_range
+    shard = args.shard if args.shard != "auto" else (
+        "interleaved" if args.gait == "mixed" else "contiguous")
+    if shard == "interleaved":
+        first, stride, _ = interleaved_shard(B, world, rank)
+    else:
+        (first, _), stride = shard_range(B, rank), 1
+    x0, xr, ft, ct = srbd.generate(SEED, N, B, args.gait, first=first, stride=stride)
     d_x0 = torch.from_numpy(x0).to(dev)
     d_xr = torch.from_numpy(xr).to(dev)
     d_ft = torch.from_numpy(ft).to(dev)
@@ -325,8 +333,8 @@ def main():
                         % (args.gait, N, B, _config_tag(N, args.gait, B)),
             "horizon": N, "batch_per_gpu": B, "gait": args.gait,
             "solver": "OSQP-algorithm ADMM, default settings (eps 1e-3, adaptive rho)",
-            "parallelism": "dp%d (instance shards, RCCL all-gather of u0%s)" % (
-                world, ", overlapped with the next solve" if overlap else ""),
+            "parallelism": "dp%d (%s instance shards, RCCL all-gather of u0%s)" % (
+                world, shard, ", overlapped with the next solve" if overlap else ""),
         },
         "p99_batch_us": round(float(np.percentile(step_ms, 99)) * 1e3, 2),
         "p50_batch_us": round(float(np.percentile(step_ms, 50)) * 1e3, 2),

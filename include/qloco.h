@@ -151,6 +151,11 @@ int qloco_srbd_build(const qloco_srbd_spec *spec, int64_t batch, const float *x0
 int qloco_gen_srbd_host(uint64_t seed, int32_t horizon, float dt, int32_t gait,
                         int64_t first, int64_t count, float *x0, float *x_ref,
                         float *feet, uint8_t *contacts);
+/* Same instances for the global ids first + k * stride, k < count (the
+ * interleaved shard of a rank: first = rank, stride = world). */
+int qloco_gen_srbd_host_strided(uint64_t seed, int32_t horizon, float dt, int32_t gait,
+                                int64_t first, int64_t stride, int64_t count, float *x0,
+                                float *x_ref, float *feet, uint8_t *contacts);
 
 /* ====================================================================== */
 /* 2. Dense small-QP active-set solver (Goldfarb-Idnani), batched.          */

@@ -68,6 +68,8 @@ SIGNATURES = {
                                    vp, vp, vp]),
     "qloco_gen_srbd_host": (C.c_int, [C.c_uint64, i32, C.c_float, i32, i64, i64, vp, vp, vp,
                                       vp]),
+    "qloco_gen_srbd_host_strided": (C.c_int, [C.c_uint64, i32, C.c_float, i32, i64, i64, i64, vp,
+                                              vp, vp, vp]),
     "qloco_eiquadprog_solve": (C.c_int, [i32, i32, i32, i64, vp, i64, vp, i64, vp, i64, vp, i64,
                                          vp, i64, vp, i64, vp, vp, vp, vp, vp]),
     "qloco_max_gi_vars": (C.c_int, []),

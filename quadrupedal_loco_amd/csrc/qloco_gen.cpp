@@ -45,13 +45,14 @@ constexpr uint8_t kPace[2][4] = {{1, 0, 1, 0}, {0, 1, 0, 1}};  // {FL,RL} / {FR,
 
 }  // namespace
 
-extern "C" int qloco_gen_srbd_host(uint64_t seed, int32_t N, float dt_f, int32_t gait, int64_t first,
-                                   int64_t count, float *x0, float *x_ref, float *feet,
-                                   uint8_t *contacts) {
-  if (N < 1 || count < 0 || !x0 || !x_ref || !feet || !contacts) return QLOCO_ERR_ARG;
+extern "C" int qloco_gen_srbd_host_strided(uint64_t seed, int32_t N, float dt_f, int32_t gait,
+                                           int64_t first, int64_t stride, int64_t count, float *x0,
+                                           float *x_ref, float *feet, uint8_t *contacts) {
+  if (N < 1 || count < 0 || stride < 1 || first < 0 || !x0 || !x_ref || !feet || !contacts)
+    return QLOCO_ERR_ARG;
   const double dt = static_cast<double>(dt_f);
   for (int64_t t = 0; t < count; ++t) {
-    const int64_t inst = first + t;
+    const int64_t inst = first + t * stride;
     const Stream S{mix64(seed + 0x9E3779B97F4A7C15ull * static_cast<uint64_t>(inst + 1))};
     const double roll = S.uniform(0, -0.1, 0.1), pitch = S.uniform(1, -0.1, 0.1);
     const double yaw = S.uniform(2, -3.141592653589793, 3.141592653589793);
@@ -96,4 +97,11 @@ extern "C" int qloco_gen_srbd_host(uint64_t seed, int32_t N, float dt_f, int32_t
     }
   }
   return QLOCO_OK;
+}
+
+extern "C" int qloco_gen_srbd_host(uint64_t seed, int32_t N, float dt_f, int32_t gait, int64_t first,
+                                   int64_t count, float *x0, float *x_ref, float *feet,
+                                   uint8_t *contacts) {
+  return qloco_gen_srbd_host_strided(seed, N, dt_f, gait, first, 1, count, x0, x_ref, feet,
+                                     contacts);
 }

@@ -2,8 +2,9 @@
 
 The SRBD instances are independent, so the path shards with no exchange
 during the solve: rank r owns the contiguous global range
-[r*B, (r+1)*B) (weak scaling, B instances per GPU) and regenerates its
-inputs locally from (seed, global id).  The only collective is one all-gather
+[r*B, (r+1)*B) (weak scaling, B instances per GPU), or the stride-interleaved
+ids r, r + world, ... (interleaved_shard), and regenerates its inputs locally
+from (seed, global id).  The only collective is one all-gather
 of the solved first-step forces u0 (12 fp32 per instance) so every rank ends
 with the whole batch's forces — a single RCCL all-gather over xGMI (backend
 "nccl" is RCCL on ROCm); the CPU tests drive the same code over gloo.
@@ -17,6 +18,17 @@ def shard_range(per_rank, rank):
     if per_rank < 0 or rank < 0:
         raise ValueError("per_rank and rank must be non-negative")
     return rank * per_rank, per_rank
+
+
+def interleaved_shard(per_rank, world, rank):
+    """Stride-interleaved shard: rank r owns the
+    global ids r, r + world, r + 2 world, ... -- (first, stride, count) for
+    srbd.generate.  Mixed per-instance schedules diverge in iteration count;
+    interleaving spreads any run of long instances in id order over all
+    ranks instead of loading one rank with it."""
+    if per_rank < 0 or rank < 0 or world < 1 or rank >= world:
+        raise ValueError("need 0 <= rank < world and per_rank >= 0")
+    return rank, world, per_rank
 
 
 def strong_shard_range(total, world, rank):
@@ -41,6 +53,16 @@ class ForceGather:
         self._flat = tdist.get_backend(group) != "gloo"
         if not self._flat:
             self._views = list(self.out.split(per_rank))
+
+    def global_order(self, out=None, interleaved=False):
+        """The gathered rows in global id order: rank order for contiguous
+        shards (the buffer itself), row k * world + r for interleaved shards
+        (a reordering copy)."""
+        out = self.out if out is None else out
+        if not interleaved:
+            return out
+        w = out.shape[1]
+        return out.view(self.world, self.per_rank, w).transpose(0, 1).reshape(-1, w)
 
     def __call__(self, u0, async_op=False):
         """Gather u0 of every rank into self.out.  async_op=True returns

@@ -37,15 +37,17 @@ def default_spec(**overrides):
     return s
 
 
-def generate(seed, horizon, count, gait="trot", first=0, dt=0.0025):
-    """Deterministic synthetic instances on the host (qloco_gen_srbd_host)."""
+def generate(seed, horizon, count, gait="trot", first=0, dt=0.0025, stride=1):
+    """Deterministic synthetic instances on the host: global ids
+    first + k * stride, k < count (qloco_gen_srbd_host_strided)."""
     g = GAITS[gait] if isinstance(gait, str) else int(gait)
     x0 = np.zeros((count, 13), np.float32)
     xr = np.zeros((count, 13 * horizon), np.float32)
     ft = np.zeros((count, 12), np.float32)
     ct = np.zeros((count, 4 * horizon), np.uint8)
-    check(lib().qloco_gen_srbd_host(seed, horizon, dt, g, first, count, ptr(x0), ptr(xr),
-                                    ptr(ft), ptr(ct)), "qloco_gen_srbd_host")
+    check(lib().qloco_gen_srbd_host_strided(seed, horizon, dt, g, first, stride, count, ptr(x0),
+                                            ptr(xr), ptr(ft), ptr(ct)),
+          "qloco_gen_srbd_host_strided")
     return x0, xr, ft, ct
 
 
