@@ -578,8 +578,17 @@ __device__ unsigned int g_phase[1 << 20];
     const uint64_t _now = __builtin_readcyclecounter();                       \
     if (t == 0 && b < (1 << 16)) g_phase[b * 16 + (i)] = (unsigned)(_now - _t0); \
   } while (0)
+// sub-phase accumulators (slots 9..15), reset at kernel entry
+#define QL_PSTAMP(v) const uint64_t v = __builtin_readcyclecounter()
+#define QL_PACC(i, v0)                                                              \
+  do {                                                                              \
+    const uint64_t _n = __builtin_readcyclecounter();                               \
+    if (t == 0 && b < (1 << 16)) g_phase[b * 16 + (i)] += (unsigned)(_n - (v0));   \
+  } while (0)
 #else
 #define QL_PHASE(i) ((void)0)
+#define QL_PSTAMP(v) ((void)0)
+#define QL_PACC(i, v0) ((void)0)
 #endif
 
 #ifndef QLOCO_SRBD_WAVES_PER_EU_W2  // two-wave kernel occupancy
@@ -615,6 +624,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
   if (b >= a.batch) return;
 #ifdef QLOCO_PHASE_TIMING
   const uint64_t _t0 = __builtin_readcyclecounter();
+  if (t == 0 && b < (1 << 16))
+    for (int i = 9; i < 16; ++i) g_phase[b * 16 + i] = 0;
 #endif
   const int N = a.N;
   const float Nf = (float)N;
@@ -921,6 +932,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
       for (int c = 0; c < NC; ++c) cnP = fmaxf(cnP, fabsf(KE(K, c)));
       const float inv_n = 1.0f / (float)(n > 0 ? n : 1);
       for (int it = 0; it < a.scaling; ++it) {
+        QL_PSTAMP(_r0);
         float cnA = fmaxf(fabsf(ra0), fabsf(ra1));
         const float zmax = fmaxf(fabsf(rz0), fabsf(rz1));
         const float zm1 = lane_prev(zmax), zm2 = lane_prev(zm1);
@@ -945,6 +957,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
         reinterpret_cast<float *>(&S.bc[buf][0])[t] = Dr;
         bsync<W>();
         float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f, t0, t1, t2, t3;
+        QL_PACC(9, _r0);
+        QL_PSTAMP(_r1);
         {
           const f4v d0 = S.bc[buf][lane & 15];
           if (W == 1 && c60) {  // padding columns: K_rc = 0 on valid rows
@@ -960,6 +974,8 @@ void srbd_admm_kernel(const SrbdArgs a) {
         }
         // row norm of D P D after this pass (without the running cost scale)
         const float cn2 = Dr * fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+        QL_PACC(10, _r1);
+        QL_PSTAMP(_r2);
         // cost scaling: mean column norm of P (= row norm, P symmetric) vs ||q||_inf
         const float sumP = bsum<W>(valid ? cn2 : 0.0f, S.red);
         float qm[1] = {valid ? fabsf(qsv) : 0.0f};
@@ -971,6 +987,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
         qsv *= ctc;
         cs *= ctc;
         cnP = cn2 * cs;
+        QL_PACC(11, _r2);
       }
       cinv = 1.0f / cs;
       const float lh0 = rl0 * rE0, uh0 = ru0 * rE0;

@@ -73,3 +73,7 @@ if __name__ == "__main__":
     for k, lab in enumerate(labels):
         print("  %-16s mean %9.0f  max %9.0f cycles" % (lab, d[:, k].mean(), d[:, k].max()))
     print("  %-16s mean %9.0f  max %9.0f cycles" % ("TOTAL", ph[:, 8].mean(), ph[:, 8].max()))
+    sub = buf.reshape(-1, 16)[:, 9:].astype(np.float64)
+    for k, lab in enumerate(["ruiz head", "ruiz absmax", "ruiz reduce", "sub12", "sub13", "sub14", "sub15"]):
+        if sub[:, k].any():
+            print("  %-16s mean %9.0f  max %9.0f cycles (sum over passes)" % (lab, sub[:, k].mean(), sub[:, k].max()))
