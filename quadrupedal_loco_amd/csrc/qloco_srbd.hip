@@ -85,8 +85,16 @@ struct SrbdLds {
   f4v bv[NC][2];           // per var: {b0,b1,b2,e0}, {e1,e2,step,comp}
   float xs[NC];            // unscaled x per var (P x)
   float Dc[NC];            // Ruiz column scaling D
-  float err[12 * kMaxN];   // per-step row values (gradient error / aggregates)
-  float Wc[12 * kMaxN];    // per-step Bqp' weights: rows 0..5 W1, rows 6..11 W0
+  union {
+    struct {
+      float err[12 * kMaxN];   // per-step row values (gradient error / aggregates)
+      float Wc[12 * kMaxN];    // per-step Bqp' weights: rows 0..5 W1, rows 6..11 W0
+      f2v k0k2[kMaxN * (kMaxN + 1)];  // [row step][col step]: horizon sums K0, K2
+    };
+    // W = 1 MFMA inverse: row <-> C-layout staging (clobbers err / Wc / k0k2;
+    // the kernel refills k0k2 after every inverse)
+    __attribute__((aligned(16))) float sc[64][20];
+  };
   float q2[16];
   float r2[12];
   float x0[16];
@@ -96,7 +104,6 @@ struct SrbdLds {
   float qs[NC];             // per var: scaled q
   int pair[NC];             // per var: 4*step + leg
   int cst[NC];              // per var: step, kMaxN on padding (row of zeros in k0k2)
-  f2v k0k2[kMaxN * (kMaxN + 1)];  // [row step][col step]: horizon sums K0, K2
   float piv[2];
   float colv[W == 1 ? 1 : 2][W == 1 ? 1 : NC];  // W = 2 inverse: pivot column
   float red[W][16];
@@ -520,6 +527,149 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1>
   bsync<1>();
 }
 
+// ---- W = 1 inverse on the matrix cores: block Gauss-Jordan.
+// K (64x64, SPD, padding rows/columns diagonal) is held as 4x4 blocks of
+// 16x16 in the C/D layout of v_mfma_f32_16x16x4_f32: lane (j, g) = 16g + j,
+// register r of block (I, J) = M[16I + 4g + r][16J + j].  Per block pivot k
+//   P = M_kk^-1 (16-pivot GJ inside the C layout), T_J = P M_kJ,
+//   M_IJ -= M_Ik T_J, M_Ik = -M_Ik P, M_kJ = T_J, M_kk = P.
+// mfma_tn(Z, Y, C) = Z^T Y + C: the A operand of 16x16x4 (lane l: A[l&15][l>>4])
+// read from a C-layout block Z gives Z^T when K-slice s takes k = 4g + s, and
+// the B operand (B[l>>4][l&15]) is register s of Y itself.  GJ on a symmetric
+// matrix keeps M_Ik = s M_kI^T (s = -1 iff exactly one of I, k is already
+// processed), so the old row block k supplies every transposed operand.
+__device__ __forceinline__ f4v mfma_tn(const f4v &Z, const f4v &Y, f4v C) {
+  C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.x, Y.x, C, 0, 0, 0);
+  C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.y, Y.y, C, 0, 0, 0);
+  C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.z, Y.z, C, 0, 0, 0);
+  C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.w, Y.w, C, 0, 0, 0);
+  return C;
+}
+__device__ __forceinline__ float f4get(const f4v &v, int r) {
+  return r == 0 ? v.x : (r == 1 ? v.y : (r == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ void f4set(f4v &v, int r, float x) {
+  if (r == 0) v.x = x; else if (r == 1) v.y = x; else if (r == 2) v.z = x; else v.w = x;
+}
+// One pivot of the in-block GJ (same entry-p trick as invert_w1): the pivot
+// row from lane (j, P/4) register P%4 by ds_bpermute, the pivot column from
+// lane P of each 16-lane row by DPP row_newbcast, the pivot by v_readlane.
+template <int P>
+__device__ __forceinline__ void cblock_pivot(f4v &B, int lane) {
+  constexpr int gq = P >> 2, rq = P & 3;
+  const float prow = f4get(B, rq);
+  const float piv = __builtin_bit_cast(
+      float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, prow), 16 * gq + P));
+  const float pinv = __builtin_amdgcn_rcpf(piv);
+  float e = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(
+                                          4 * (16 * gq + (lane & 15)), __builtin_bit_cast(int, prow)));
+  e = ((lane & 15) == P) ? piv + 1.0f : e;
+  const bool pgrp = (lane >> 4) == gq;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float c = dpp<0x150 + P>(f4get(B, r));  // M[4g + r][P]
+    float g = c * pinv;
+    if (r == rq) g = pgrp ? (1.0f - pinv) : g;
+    f4set(B, r, fmaf(-g, e, f4get(B, r)));
+  }
+}
+__device__ __forceinline__ void cblock_inverse(f4v &B, int lane) {
+  cblock_pivot<0>(B, lane); cblock_pivot<1>(B, lane); cblock_pivot<2>(B, lane);
+  cblock_pivot<3>(B, lane); cblock_pivot<4>(B, lane); cblock_pivot<5>(B, lane);
+  cblock_pivot<6>(B, lane); cblock_pivot<7>(B, lane); cblock_pivot<8>(B, lane);
+  cblock_pivot<9>(B, lane); cblock_pivot<10>(B, lane); cblock_pivot<11>(B, lane);
+  cblock_pivot<12>(B, lane); cblock_pivot<13>(B, lane); cblock_pivot<14>(B, lane);
+  cblock_pivot<15>(B, lane);
+}
+template <int k>
+__device__ __forceinline__ void gj_block_step(f4v (&M)[4][4], int lane) {
+  cblock_inverse(M[k][k], lane);
+  const f4v P = M[k][k];
+  f4v O[4], T[4];
+#pragma unroll
+  for (int J = 0; J < 4; ++J) O[J] = M[k][J];
+#pragma unroll
+  for (int J = 0; J < 4; ++J)
+    if (J != k) T[J] = mfma_tn(P, O[J], (f4v)(0.0f));  // P symmetric: P^T = P
+  // rows already processed: M_Ik = -O_I^T
+#pragma unroll
+  for (int I = 0; I < k; ++I) {
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+      if (J != k) M[I][J] = mfma_tn(O[I], T[J], M[I][J]);
+    M[I][k] = mfma_tn(O[I], P, (f4v)(0.0f));
+  }
+  // rows not yet processed: M_Ik = +O_I^T
+#pragma unroll
+  for (int J = 0; J < 4; ++J)
+    if (J != k) T[J] = -T[J];
+  const f4v nP = -P;
+#pragma unroll
+  for (int I = k + 1; I < 4; ++I) {
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+      if (J != k) M[I][J] = mfma_tn(O[I], T[J], M[I][J]);
+    M[I][k] = mfma_tn(O[I], nP, (f4v)(0.0f));
+  }
+#pragma unroll
+  for (int J = 0; J < 4; ++J)
+    if (J != k) M[k][J] = -T[J];
+}
+// Row layout in and out (lane v holds row v of K, then of K^-1).  K and
+// K^-1 are symmetric, so block (I, J) of the C layout is row 16J + j,
+// columns 16I + 4g.. +3: one 16-byte LDS access per block and lane.
+// Block pivots past the valid columns (ncol) are identity-padding blocks
+// and are skipped (their rows / columns carry zeros off the diagonal).
+__device__ __forceinline__ void invert_w1_mfma(SrbdLds<1> &S, int t, int ncol, Row<1> &K) {
+  const int lane = t & 63, j = lane & 15, g = lane >> 4;
+  const int nb = (__builtin_amdgcn_readfirstlane(ncol) + 15) >> 4;
+  f4v M[4][4];
+  bsync<1>();
+#pragma unroll
+  for (int I = 0; I < 4; ++I) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<f4v *>(&S.sc[lane][4 * q]) =
+          (f4v){K.k[16 * I + 4 * q], K.k[16 * I + 4 * q + 1], K.k[16 * I + 4 * q + 2],
+                K.k[16 * I + 4 * q + 3]};
+    bsync<1>();
+#pragma unroll
+    for (int J = 0; J < 4; ++J) M[I][J] = *reinterpret_cast<const f4v *>(&S.sc[16 * J + j][4 * g]);
+    bsync<1>();
+  }
+  gj_block_step<0>(M, lane);
+  if (nb > 1) gj_block_step<1>(M, lane);
+  if (nb > 2) gj_block_step<2>(M, lane);
+  if (nb > 3) gj_block_step<3>(M, lane);
+#pragma unroll
+  for (int I = 0; I < 4; ++I) {
+#pragma unroll
+    for (int J = 0; J < 4; ++J) *reinterpret_cast<f4v *>(&S.sc[16 * J + j][4 * g]) = M[I][J];
+    bsync<1>();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f4v v = *reinterpret_cast<const f4v *>(&S.sc[lane][4 * q]);
+      K.k[16 * I + 4 * q] = v.x;
+      K.k[16 * I + 4 * q + 1] = v.y;
+      K.k[16 * I + 4 * q + 2] = v.z;
+      K.k[16 * I + 4 * q + 3] = v.w;
+    }
+    bsync<1>();
+  }
+}
+
+// K0 / K2 table over (row step, column step); column kMaxN is the zero row
+// of padding lanes (cst = kMaxN)
+template <int W>
+__device__ __forceinline__ void fill_k0k2(SrbdLds<W> &S, int N, float Nf, int t) {
+  for (int idx = t; idx < N * (kMaxN + 1); idx += 64 * W) {
+    const int sr = idx / (kMaxN + 1), sc = idx - (kMaxN + 1) * sr;
+    float K0 = 0.0f, K2 = 0.0f;
+    if (sc < N) k0k2((float)sr, (float)sc, Nf, K0, K2);
+    S.k0k2[idx] = (f2v){K0, K2};
+  }
+}
+
 
 // Two-wave form: the same transposed write, one pivot half per wave (the
 // pivot column register is static inside each half), one s_barrier per
@@ -712,12 +862,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
     leg = pair & 3;
   }
   S.cst[t] = valid ? step : kMaxN;
-  for (int idx = t; idx < N * (kMaxN + 1); idx += 64 * W) {
-    const int sr = idx / (kMaxN + 1), sc = idx - (kMaxN + 1) * sr;
-    float K0 = 0.0f, K2 = 0.0f;
-    if (sc < N) k0k2((float)sr, (float)sc, Nf, K0, K2);
-    S.k0k2[idx] = (f2v){K0, K2};
-  }
+  fill_k0k2<W>(S, N, Nf, t);
 
   QL_PHASE(1);
   // ---------------- 3. SRBD model terms (ConvexMpc.cpp:111-160, compute_grf :502-549)
@@ -1023,15 +1168,22 @@ void srbd_admm_kernel(const SrbdArgs a) {
       if (first) QL_PHASE(5);
       if constexpr (W == 1) {
         (void)dg;
+#ifdef QLOCO_SRBD_DPP_INV  // the register-row DPP Gauss-Jordan (comparison builds)
         if (c60) {
           invert_w1<true>(S, t, ncol[0], K);
-#ifdef QLOCO_ABLATE_DUP_INV  // timing experiments only: K^-1 -> K -> K^-1
-          invert_w1<true>(S, t, ncol[0], K);
-          invert_w1<true>(S, t, ncol[0], K);
-#endif
         } else {
           invert_w1<false>(S, t, ncol[0], K);
         }
+#else
+        invert_w1_mfma(S, t, ncol[0], K);
+#ifdef QLOCO_ABLATE_DUP_INV  // timing experiments only: K^-1 -> K -> K^-1
+        invert_w1_mfma(S, t, ncol[0], K);
+        invert_w1_mfma(S, t, ncol[0], K);
+#endif
+        // the staging buffer overlaid the K0 / K2 table
+        fill_k0k2<1>(S, N, Nf, t);
+        bsync<1>();
+#endif
       } else {
         (void)dg;
         invert_w2(S, t, ncol, c2, K);

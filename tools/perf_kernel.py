@@ -19,6 +19,9 @@ VARIANTS = {
     # 150 iterations with 30 residual checks that never pass (eps 1e-12): check cost
     "chk5": dict(max_iter=150, check_termination=5, adaptive_rho=0, eps_abs=1e-12, eps_rel=1e-12),
     "iter150": dict(max_iter=150, check_termination=0, adaptive_rho=0),
+    "iter150s0": dict(max_iter=150, check_termination=0, adaptive_rho=0, scaling=0),
+    "iter0": dict(max_iter=0, check_termination=0, adaptive_rho=0),
+    "iter0s0": dict(max_iter=0, check_termination=0, adaptive_rho=0, scaling=0),
     "rho25": dict(max_iter=150, eps_abs=1e-12, eps_rel=1e-12, adaptive_rho=1,
                   adaptive_rho_interval=25, adaptive_rho_tolerance=1.0),
 }
