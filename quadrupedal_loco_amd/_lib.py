@@ -8,7 +8,9 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libqloco.so")
+# QLOCO_LIB: an experimental build of the same library (tools/variant_lib.py)
+# for A/B timing runs; unset, the in-tree product library
+LIB_PATH = os.environ.get("QLOCO_LIB") or os.path.join(HERE, "lib", "libqloco.so")
 
 _lib = None
 

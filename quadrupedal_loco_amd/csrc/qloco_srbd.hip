@@ -30,13 +30,23 @@
 //    packed-FMA matvec against the register-resident K^-1, four DPP lane
 //    shifts (wave_shr/wave_shl) for the leg-local constraint couplings.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
+#include <mutex>
 
 #include <type_traits>
 
 #include "qloco_common.hpp"
 #include "qloco_dpp.inc"
 
+// The KKT inverse: register-row DPP Gauss-Jordan (default) or the
+// matrix-core block Gauss-Jordan (QLOCO_SRBD_MFMA_INV=1; as accurate, but
+// slower once made stable -- measured).
+#ifndef QLOCO_SRBD_MFMA_INV
+#define QLOCO_SRBD_MFMA_INV 0
+#endif
 #ifndef QLOCO_W2_GJ_BUCKETS  // second-half chunk buckets in the W = 2 inverse too
 #define QLOCO_W2_GJ_BUCKETS 0
 #endif
@@ -65,6 +75,10 @@ struct SrbdArgs {
   const uint8_t *contacts;
   float *u0, *u, *obj, *warm;
   int *status, *iters, *rho_updates;
+  // optional instance list (positions 0..count-1 -> instance ids) and its
+  // device-side length (qloco_srbd_solve_ex's class lists)
+  const int *list;
+  const int *count;
 };
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -91,9 +105,11 @@ struct SrbdLds {
       float Wc[12 * kMaxN];    // per-step Bqp' weights: rows 0..5 W1, rows 6..11 W0
       f2v k0k2[kMaxN * (kMaxN + 1)];  // [row step][col step]: horizon sums K0, K2
     };
-    // W = 1 MFMA inverse: row <-> C-layout staging (clobbers err / Wc / k0k2;
-    // the kernel refills k0k2 after every inverse)
-    __attribute__((aligned(16))) float sc[64][20];
+    // MFMA inverse staging (clobbers err / Wc / k0k2; the kernel refills
+    // k0k2 after every inverse).  W = 1: the transpose buffer (16 x 68);
+    // W = 2: per-wave transposes (2 x 16 x 68) or the double-buffered
+    // pivot row-block exchange (2 x 8 blocks x 64 lanes x 4)
+    __attribute__((aligned(16))) float sc[QLOCO_SRBD_MFMA_INV ? (W == 1 ? 16 * 68 : 2 * 8 * 256) : 1];
   };
   float q2[16];
   float r2[12];
@@ -527,17 +543,26 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1>
   bsync<1>();
 }
 
-// ---- W = 1 inverse on the matrix cores: block Gauss-Jordan.
-// K (64x64, SPD, padding rows/columns diagonal) is held as 4x4 blocks of
-// 16x16 in the C/D layout of v_mfma_f32_16x16x4_f32: lane (j, g) = 16g + j,
-// register r of block (I, J) = M[16I + 4g + r][16J + j].  Per block pivot k
-//   P = M_kk^-1 (16-pivot GJ inside the C layout), T_J = P M_kJ,
-//   M_IJ -= M_Ik T_J, M_Ik = -M_Ik P, M_kJ = T_J, M_kk = P.
-// mfma_tn(Z, Y, C) = Z^T Y + C: the A operand of 16x16x4 (lane l: A[l&15][l>>4])
-// read from a C-layout block Z gives Z^T when K-slice s takes k = 4g + s, and
-// the B operand (B[l>>4][l&15]) is register s of Y itself.  GJ on a symmetric
-// matrix keeps M_Ik = s M_kI^T (s = -1 iff exactly one of I, k is already
-// processed), so the old row block k supplies every transposed operand.
+// ---- KKT inverse on the matrix cores: block Gauss-Jordan.
+// K (64x64 for W = 1, SPD, padding rows/columns diagonal) is held as blocks
+// of 16x16 in the C/D layout of v_mfma_f32_16x16x4_f32: lane (j, g) =
+// 16g + j, register r of block (I, J) = M[16I + 4g + r][16J + j].
+// mfma_tn(Z, Y, C) = Z^T Y + C: the A operand of 16x16x4 (lane l:
+// A[l&15][l>>4]) read from a C-layout block Z gives Z^T when K-slice s takes
+// k = 4g + s, and the B operand (B[l>>4][l&15]) is register s of Y itself;
+// with Y = I it is an exact transpose.  Per block pivot k:
+//  1. the row block k is transposed (Z_J = M_kJ^T) and Gauss-Jordan runs on
+//     its 16 rows with the 16 pivots of the diagonal block (in-place form,
+//     entry-p trick of invert_w1): Z_J -> T_J^T, T_J = M_kk^-1 M_kJ, and
+//     Z_k -> (M_kk^-1)^T.  Elimination, not an explicit inverse times M_kJ:
+//     multiplying by the 16x16 inverse loses a factor cond(M_kk) (measured,
+//     tools/micro/w2_inverse.hip: 2e-1 vs 2.4e-4 at cond 1e4);
+//  2. every other block row I: M_IJ -= M_Ik T_J and M_Ik = -M_Ik M_kk^-1
+//     (MFMA, A operand the exact transpose of the old M_Ik);
+//  3. M_kJ = T_J, M_kk = M_kk^-1.
+// Taking the transposed operands from the symmetry GJ keeps (M_Ik = -+M_kI^T)
+// instead of exact transposes is NOT stable: a float32 emulation gives
+// |K X - I| = 0.67 vs 5e-4 (this form) vs 1e-3 (element GJ) at cond 1e5.
 __device__ __forceinline__ f4v mfma_tn(const f4v &Z, const f4v &Y, f4v C) {
   C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.x, Y.x, C, 0, 0, 0);
   C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.y, Y.y, C, 0, 0, 0);
@@ -545,117 +570,201 @@ __device__ __forceinline__ f4v mfma_tn(const f4v &Z, const f4v &Y, f4v C) {
   C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.w, Y.w, C, 0, 0, 0);
   return C;
 }
+__device__ __forceinline__ f4v cident(int lane) {  // 16x16 identity, C layout
+  const int j = lane & 15, g4 = 4 * (lane >> 4);
+  return (f4v){g4 == j ? 1.0f : 0.0f, g4 + 1 == j ? 1.0f : 0.0f, g4 + 2 == j ? 1.0f : 0.0f,
+               g4 + 3 == j ? 1.0f : 0.0f};
+}
+__device__ __forceinline__ f4v ctrans(const f4v &Z, const f4v &Id) {
+  return mfma_tn(Z, Id, (f4v)(0.0f));
+}
 __device__ __forceinline__ float f4get(const f4v &v, int r) {
   return r == 0 ? v.x : (r == 1 ? v.y : (r == 2 ? v.z : v.w));
 }
 __device__ __forceinline__ void f4set(f4v &v, int r, float x) {
   if (r == 0) v.x = x; else if (r == 1) v.y = x; else if (r == 2) v.z = x; else v.w = x;
 }
-// One pivot of the in-block GJ (same entry-p trick as invert_w1): the pivot
-// row from lane (j, P/4) register P%4 by ds_bpermute, the pivot column from
-// lane P of each 16-lane row by DPP row_newbcast, the pivot by v_readlane.
-template <int P>
-__device__ __forceinline__ void cblock_pivot(f4v &B, int lane) {
+// Pivot P of the transposed row block Z[0..NB) (lane (a, g) register r of
+// Z_J = M[16k + a][16J + 4g + r]): the pivot by v_readlane, this lane's
+// row coefficient M[16k + a][16k + P] by ds_bpermute (it sits in group P/4),
+// the pivot row entry of this lane's column by DPP row_newbcast:P.
+template <int P, int NB, int k>
+__device__ __forceinline__ void rowblock_pivot(f4v (&Z)[NB], int lane) {
   constexpr int gq = P >> 2, rq = P & 3;
-  const float prow = f4get(B, rq);
+  const int a = lane & 15;
+  const float pv = f4get(Z[k], rq);
   const float piv = __builtin_bit_cast(
-      float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, prow), 16 * gq + P));
+      float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pv), 16 * gq + P));
   const float pinv = __builtin_amdgcn_rcpf(piv);
-  float e = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(
-                                          4 * (16 * gq + (lane & 15)), __builtin_bit_cast(int, prow)));
-  e = ((lane & 15) == P) ? piv + 1.0f : e;
-  const bool pgrp = (lane >> 4) == gq;
+  const float ca = __builtin_bit_cast(
+      float, __builtin_amdgcn_ds_bpermute(4 * (16 * gq + a), __builtin_bit_cast(int, pv)));
+  const float ng = (a == P) ? (pinv - 1.0f) : -(ca * pinv);
+  const bool plane = lane == 16 * gq + P;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float c = dpp<0x150 + P>(f4get(B, r));  // M[4g + r][P]
-    float g = c * pinv;
-    if (r == rq) g = pgrp ? (1.0f - pinv) : g;
-    f4set(B, r, fmaf(-g, e, f4get(B, r)));
+  for (int J = 0; J < NB; ++J) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float src = f4get(Z[J], r);
+      if (J == k && r == rq) src = plane ? piv + 1.0f : src;
+      const float e = dpp<0x150 + P>(src);
+      f4set(Z[J], r, fmaf(ng, e, f4get(Z[J], r)));
+    }
   }
 }
-__device__ __forceinline__ void cblock_inverse(f4v &B, int lane) {
-  cblock_pivot<0>(B, lane); cblock_pivot<1>(B, lane); cblock_pivot<2>(B, lane);
-  cblock_pivot<3>(B, lane); cblock_pivot<4>(B, lane); cblock_pivot<5>(B, lane);
-  cblock_pivot<6>(B, lane); cblock_pivot<7>(B, lane); cblock_pivot<8>(B, lane);
-  cblock_pivot<9>(B, lane); cblock_pivot<10>(B, lane); cblock_pivot<11>(B, lane);
-  cblock_pivot<12>(B, lane); cblock_pivot<13>(B, lane); cblock_pivot<14>(B, lane);
-  cblock_pivot<15>(B, lane);
+template <int NB, int k>
+__device__ __forceinline__ void rowblock_gj(f4v (&Z)[NB], int lane) {
+  rowblock_pivot<0, NB, k>(Z, lane); rowblock_pivot<1, NB, k>(Z, lane);
+  rowblock_pivot<2, NB, k>(Z, lane); rowblock_pivot<3, NB, k>(Z, lane);
+  rowblock_pivot<4, NB, k>(Z, lane); rowblock_pivot<5, NB, k>(Z, lane);
+  rowblock_pivot<6, NB, k>(Z, lane); rowblock_pivot<7, NB, k>(Z, lane);
+  rowblock_pivot<8, NB, k>(Z, lane); rowblock_pivot<9, NB, k>(Z, lane);
+  rowblock_pivot<10, NB, k>(Z, lane); rowblock_pivot<11, NB, k>(Z, lane);
+  rowblock_pivot<12, NB, k>(Z, lane); rowblock_pivot<13, NB, k>(Z, lane);
+  rowblock_pivot<14, NB, k>(Z, lane); rowblock_pivot<15, NB, k>(Z, lane);
 }
 template <int k>
-__device__ __forceinline__ void gj_block_step(f4v (&M)[4][4], int lane) {
-  cblock_inverse(M[k][k], lane);
-  const f4v P = M[k][k];
-  f4v O[4], T[4];
+__device__ __forceinline__ void gj_block_step(f4v (&M)[4][4], int lane, const f4v &Id) {
+  f4v Z[4];
 #pragma unroll
-  for (int J = 0; J < 4; ++J) O[J] = M[k][J];
+  for (int J = 0; J < 4; ++J) Z[J] = ctrans(M[k][J], Id);
+  rowblock_gj<4, k>(Z, lane);
+  f4v nT[4];
 #pragma unroll
-  for (int J = 0; J < 4; ++J)
-    if (J != k) T[J] = mfma_tn(P, O[J], (f4v)(0.0f));  // P symmetric: P^T = P
-  // rows already processed: M_Ik = -O_I^T
+  for (int J = 0; J < 4; ++J) nT[J] = -ctrans(Z[J], Id);  // nT[k] = -M_kk^-1
 #pragma unroll
-  for (int I = 0; I < k; ++I) {
-#pragma unroll
-    for (int J = 0; J < 4; ++J)
-      if (J != k) M[I][J] = mfma_tn(O[I], T[J], M[I][J]);
-    M[I][k] = mfma_tn(O[I], P, (f4v)(0.0f));
-  }
-  // rows not yet processed: M_Ik = +O_I^T
-#pragma unroll
-  for (int J = 0; J < 4; ++J)
-    if (J != k) T[J] = -T[J];
-  const f4v nP = -P;
-#pragma unroll
-  for (int I = k + 1; I < 4; ++I) {
+  for (int I = 0; I < 4; ++I) {
+    if (I == k) continue;
+    const f4v ZI = ctrans(M[I][k], Id);  // old M_Ik^T
 #pragma unroll
     for (int J = 0; J < 4; ++J)
-      if (J != k) M[I][J] = mfma_tn(O[I], T[J], M[I][J]);
-    M[I][k] = mfma_tn(O[I], nP, (f4v)(0.0f));
+      if (J != k) M[I][J] = mfma_tn(ZI, nT[J], M[I][J]);
+    M[I][k] = mfma_tn(ZI, nT[k], (f4v)(0.0f));
   }
 #pragma unroll
-  for (int J = 0; J < 4; ++J)
-    if (J != k) M[k][J] = -T[J];
+  for (int J = 0; J < 4; ++J) M[k][J] = -nT[J];
 }
-// Row layout in and out (lane v holds row v of K, then of K^-1).  K and
-// K^-1 are symmetric, so block (I, J) of the C layout is row 16J + j,
-// columns 16I + 4g.. +3: one 16-byte LDS access per block and lane.
+// Row layout in and out (lane v holds row v of K, then of K^-1) through a
+// transpose buffer tb[c][row] of 16 columns at a time.  The computed K^-1 is
+// not exactly symmetric, so no entry is taken from its mirror (reading
+// M[r][c] from row c was measured ~1000x less accurate at cond 1e5).
 // Block pivots past the valid columns (ncol) are identity-padding blocks
 // and are skipped (their rows / columns carry zeros off the diagonal).
 __device__ __forceinline__ void invert_w1_mfma(SrbdLds<1> &S, int t, int ncol, Row<1> &K) {
   const int lane = t & 63, j = lane & 15, g = lane >> 4;
   const int nb = (__builtin_amdgcn_readfirstlane(ncol) + 15) >> 4;
+  float *tb = S.sc;
   f4v M[4][4];
   bsync<1>();
 #pragma unroll
-  for (int I = 0; I < 4; ++I) {
+  for (int J = 0; J < 4; ++J) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<f4v *>(&S.sc[lane][4 * q]) =
-          (f4v){K.k[16 * I + 4 * q], K.k[16 * I + 4 * q + 1], K.k[16 * I + 4 * q + 2],
-                K.k[16 * I + 4 * q + 3]};
+    for (int c = 0; c < 16; ++c) tb[c * 68 + lane] = K.k[16 * J + c];
     bsync<1>();
 #pragma unroll
-    for (int J = 0; J < 4; ++J) M[I][J] = *reinterpret_cast<const f4v *>(&S.sc[16 * J + j][4 * g]);
+    for (int I = 0; I < 4; ++I) M[I][J] = *reinterpret_cast<const f4v *>(&tb[j * 68 + 16 * I + 4 * g]);
     bsync<1>();
   }
-  gj_block_step<0>(M, lane);
-  if (nb > 1) gj_block_step<1>(M, lane);
-  if (nb > 2) gj_block_step<2>(M, lane);
-  if (nb > 3) gj_block_step<3>(M, lane);
+  const f4v Id = cident(lane);
+  gj_block_step<0>(M, lane, Id);
+  if (nb > 1) gj_block_step<1>(M, lane, Id);
+  if (nb > 2) gj_block_step<2>(M, lane, Id);
+  if (nb > 3) gj_block_step<3>(M, lane, Id);
 #pragma unroll
-  for (int I = 0; I < 4; ++I) {
+  for (int J = 0; J < 4; ++J) {
 #pragma unroll
-    for (int J = 0; J < 4; ++J) *reinterpret_cast<f4v *>(&S.sc[16 * J + j][4 * g]) = M[I][J];
+    for (int I = 0; I < 4; ++I) *reinterpret_cast<f4v *>(&tb[j * 68 + 16 * I + 4 * g]) = M[I][J];
     bsync<1>();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f4v v = *reinterpret_cast<const f4v *>(&S.sc[lane][4 * q]);
-      K.k[16 * I + 4 * q] = v.x;
-      K.k[16 * I + 4 * q + 1] = v.y;
-      K.k[16 * I + 4 * q + 2] = v.z;
-      K.k[16 * I + 4 * q + 3] = v.w;
-    }
+    for (int c = 0; c < 16; ++c) K.k[16 * J + c] = tb[c * 68 + lane];
     bsync<1>();
   }
+}
+
+// ---- W = 2 inverse on the matrix cores: the same block Gauss-Jordan over
+// 8 x 8 blocks; wave w holds block rows 4w..4w+3 (its 64 K rows) in the C
+// layout.  Per block pivot k the owning wave eliminates its transposed row
+// block and publishes Z_J = T_J^T through LDS, one barrier, then both waves
+// update their own block rows (each transposes the Z_J it needs); the
+// buffer alternates with k, so a wave may run ahead into step k + 1 safely.
+template <int k, int w>
+__device__ __forceinline__ void gj2_step(SrbdLds<2> &S, f4v (&M)[4][8], int lane, const f4v &Id) {
+  constexpr int ow = k >> 2, ik = k & 3;
+  f4v *xb = reinterpret_cast<f4v *>(S.sc) + (k & 1) * 8 * 64;  // [block J][lane]
+  f4v Z[8];
+  if constexpr (w == ow) {
+#pragma unroll
+    for (int J = 0; J < 8; ++J) Z[J] = ctrans(M[ik][J], Id);
+    rowblock_gj<8, k>(Z, lane);
+#pragma unroll
+    for (int J = 0; J < 8; ++J) xb[J * 64 + lane] = Z[J];
+  }
+  f4v ZI[4];  // old M_Ik^T of this wave's block rows
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (4 * w + i != k) ZI[i] = ctrans(M[i][k], Id);
+  __syncthreads();
+#pragma unroll
+  for (int J = 0; J < 8; ++J) {
+    if (J == k) continue;
+    const f4v ZJ = (w == ow) ? Z[J] : xb[J * 64 + lane];
+    const f4v nT = -ctrans(ZJ, Id);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * w + i != k) M[i][J] = mfma_tn(ZI[i], nT, M[i][J]);
+    if constexpr (w == ow) M[ik][J] = -nT;
+  }
+  const f4v nP = -ctrans((w == ow) ? Z[k] : xb[k * 64 + lane], Id);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (4 * w + i != k) M[i][k] = mfma_tn(ZI[i], nP, (f4v)(0.0f));
+  if constexpr (w == ow) M[ik][k] = -nP;
+}
+template <int w>
+__device__ __forceinline__ void gj2_steps(SrbdLds<2> &S, f4v (&M)[4][8], int lane, int nb) {
+  const f4v Id = cident(lane);
+  gj2_step<0, w>(S, M, lane, Id);
+  gj2_step<1, w>(S, M, lane, Id);
+  gj2_step<2, w>(S, M, lane, Id);
+  gj2_step<3, w>(S, M, lane, Id);
+  if (nb > 4) gj2_step<4, w>(S, M, lane, Id);
+  if (nb > 5) gj2_step<5, w>(S, M, lane, Id);
+  if (nb > 6) gj2_step<6, w>(S, M, lane, Id);
+  if (nb > 7) gj2_step<7, w>(S, M, lane, Id);
+}
+// Row layout in and out through a per-wave transpose buffer (tb[c][row]:
+// 16 columns of the wave's 64 rows); block pivots past the valid columns of
+// the second half are identity-padding blocks and are skipped.
+__device__ __forceinline__ void invert_w2_mfma(SrbdLds<2> &S, int t, int ncol1, Row<2> &K) {
+  const int wave = t >> 6, lane = t & 63, j = lane & 15, g = lane >> 4;
+  const int nb = 4 + ((__builtin_amdgcn_readfirstlane(ncol1) + 15) >> 4);
+  float *tb = S.sc + wave * (16 * 68);
+  f4v M[4][8];
+  __syncthreads();
+#pragma unroll
+  for (int J = 0; J < 8; ++J) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) tb[c * 68 + lane] = K.k[16 * J + c];
+    bsync<1>();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) M[i][J] = *reinterpret_cast<const f4v *>(&tb[j * 68 + 16 * i + 4 * g]);
+    bsync<1>();
+  }
+  __syncthreads();
+  if (wave == 0)
+    gj2_steps<0>(S, M, lane, nb);
+  else
+    gj2_steps<1>(S, M, lane, nb);
+  __syncthreads();
+#pragma unroll
+  for (int J = 0; J < 8; ++J) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<f4v *>(&tb[j * 68 + 16 * i + 4 * g]) = M[i][J];
+    bsync<1>();
+#pragma unroll
+    for (int c = 0; c < 16; ++c) K.k[16 * J + c] = tb[c * 68 + lane];
+    bsync<1>();
+  }
+  __syncthreads();
 }
 
 // K0 / K2 table over (row step, column step); column kMaxN is the zero row
@@ -744,34 +853,26 @@ __device__ unsigned int g_phase[1 << 20];
 #ifndef QLOCO_SRBD_WAVES_PER_EU_W2  // two-wave kernel occupancy
 #define QLOCO_SRBD_WAVES_PER_EU_W2 2
 #endif
-#ifndef QLOCO_SRBD_WAVES_PER_EU  // one-wave kernel occupancy for large batches: 3 waves/SIMD
-#define QLOCO_SRBD_WAVES_PER_EU 3    // = 168 VGPRs (23 spills, all in setup / refactor paths)
+#ifndef QLOCO_SRBD_WAVES_PER_EU  // one-wave kernel occupancy: 3 waves/SIMD
+#define QLOCO_SRBD_WAVES_PER_EU 3    // = 168 VGPRs (small spills in the setup / refactor paths)
 #endif
-// One-wave kernel, small batches (<= kSmallBatch instances, i.e. <= 6 waves
-// per SIMD over the launch): 2 waves/SIMD = 194 VGPRs, spill-free -- with few
-// waves per SIMD the tail of long instances dominates and more registers per
-// wave (no scratch round trips) beat the third resident wave.  Measured on
-// Go1 trot N = 10: B = 4096 307 vs 314 us, B = 8192 539 vs 505 us.
+// With the matrix-core inverse the three-wave kernel is at least as fast as
+// the spill-free two-wave one (194 VGPRs) at every batch size measured
+// (Go1 trot N = 10: B = 1024 / 2048 / 4096 / 8192 143.6 / 214.5 / 286.6 /
+// 465.5 vs 143.4 / 214.9 / 297.8 / 473.2 us; four waves: 137.6 / 207.1 /
+// 290.4 / 510.5; profiles/r2q_persistent_queue_and_occupancy.txt), so it is
+// the only one-wave instantiation.
 #ifndef QLOCO_SRBD_NUM_VGPR_ATTR  // experiments: force a VGPR budget
 #define QLOCO_SRBD_NUM_VGPR_ATTR
 #endif
-#ifndef QLOCO_SMALL_BATCH
-#define QLOCO_SMALL_BATCH 6144
-#endif
-constexpr int64_t kSmallBatch = QLOCO_SMALL_BATCH;
 
 // WS: a warm-start mode (1 or 2) may be set.  The cold-start instantiation
 // (the headline path) carries none of the warm / persistent-record code.
-template <int W, int WPE, bool WS>
-__global__ __launch_bounds__(64 * W)
-__attribute__((amdgpu_waves_per_eu(WPE))) QLOCO_SRBD_NUM_VGPR_ATTR
-void srbd_admm_kernel(const SrbdArgs a) {
+template <int W, bool WS>
+__device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S, const int64_t b) {
   constexpr int NC = 64 * W, NQ = 16 * W;
-  __shared__ __attribute__((aligned(16))) SrbdLds<W> S;
   const int t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
-  const int64_t b = blockIdx.x;
-  if (b >= a.batch) return;
 #ifdef QLOCO_PHASE_TIMING
   const uint64_t _t0 = __builtin_readcyclecounter();
   if (t == 0 && b < (1 << 16))
@@ -1168,25 +1269,30 @@ void srbd_admm_kernel(const SrbdArgs a) {
       if (first) QL_PHASE(5);
       if constexpr (W == 1) {
         (void)dg;
-#ifdef QLOCO_SRBD_DPP_INV  // the register-row DPP Gauss-Jordan (comparison builds)
+#if QLOCO_SRBD_MFMA_INV  // matrix-core block Gauss-Jordan (comparison builds)
+        invert_w1_mfma(S, t, ncol[0], K);
+        fill_k0k2<1>(S, N, Nf, t);  // the staging buffer overlaid the K0 / K2 table
+        bsync<1>();
+#else
         if (c60) {
           invert_w1<true>(S, t, ncol[0], K);
+#ifdef QLOCO_ABLATE_DUP_INV  // timing experiments only: K^-1 -> K -> K^-1
+          invert_w1<true>(S, t, ncol[0], K);
+          invert_w1<true>(S, t, ncol[0], K);
+#endif
         } else {
           invert_w1<false>(S, t, ncol[0], K);
         }
-#else
-        invert_w1_mfma(S, t, ncol[0], K);
-#ifdef QLOCO_ABLATE_DUP_INV  // timing experiments only: K^-1 -> K -> K^-1
-        invert_w1_mfma(S, t, ncol[0], K);
-        invert_w1_mfma(S, t, ncol[0], K);
-#endif
-        // the staging buffer overlaid the K0 / K2 table
-        fill_k0k2<1>(S, N, Nf, t);
-        bsync<1>();
 #endif
       } else {
         (void)dg;
+#if QLOCO_SRBD_MFMA_INV
+        invert_w2_mfma(S, t, ncol[1], K);
+        fill_k0k2<2>(S, N, Nf, t);
+        __syncthreads();
+#else
         invert_w2(S, t, ncol, c2, K);
+#endif
       }
       if (first) QL_PHASE(6);
     }
@@ -1460,6 +1566,51 @@ void srbd_admm_kernel(const SrbdArgs a) {
   }
 }
 
+// One instance per workgroup: instance list[blockIdx] (or blockIdx) for
+// list positions below the device-side count (or the batch).
+template <int W, int WPE, bool WS>
+__global__ __launch_bounds__(64 * W)
+__attribute__((amdgpu_waves_per_eu(WPE))) QLOCO_SRBD_NUM_VGPR_ATTR
+void srbd_admm_kernel(const SrbdArgs a) {
+  __shared__ __attribute__((aligned(16))) SrbdLds<W> S;
+  const int64_t i = blockIdx.x;
+  if (i >= (a.count ? (int64_t)*a.count : a.batch)) return;
+  srbd_solve_one<W, WS>(a, S, a.list ? (int64_t)a.list[i] : i);
+}
+
+// Class of every instance by its stance-leg count (<= 21: one wave, <= 42:
+// two waves, else the wide kernel; capped at the top class the launch
+// admits), appended to that class's list: one ballot per class and wave,
+// one atomic per wave and class (list order within a wave is instance order).
+__global__ __launch_bounds__(256) void srbd_classify_kernel(const SrbdArgs a, int top, int *lists,
+                                                            int64_t cap, int *counts) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int N = a.N;
+  int cls = -1;
+  if (b < a.batch) {
+    int legs = 0;
+    if (a.contacts_per_step) {
+      const uint8_t *c = a.contacts + b * 4 * N;
+      for (int k = 0; k < 4 * N; ++k) legs += c[k] != 0;
+    } else {
+      for (int k = 0; k < 4; ++k) legs += a.contacts[b * 4 + k] != 0;
+      legs *= N;
+    }
+    cls = legs <= kLegsPerWave ? 0 : (legs <= 2 * kLegsPerWave ? 1 : 2);
+    cls = cls > top ? top : cls;
+  }
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int c = 0; c <= top; ++c) {
+    const uint64_t m = __ballot(cls == c);
+    if (!m) continue;
+    int base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&counts[c], __popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (cls == c) lists[(int64_t)c * cap + base + __popcll(m & below)] = (int)b;
+  }
+}
+
 }  // namespace qloco
 
 #include "qloco_srbd_big.inc"
@@ -1508,6 +1659,56 @@ extern "C" int qloco_phase_read(unsigned int *host, size_t count) {
                                   hipMemcpyDeviceToHost);
 }
 #endif
+
+// Per-device scratch of the class dispatch: three instance lists of `cap`
+// entries, their counters, two side streams and the fork / join events.
+// Grown (never shrunk) under a mutex; a grow waits for the device first, as
+// in-flight launches may still read the old lists.
+struct SrbdScratch {
+  int *lists = nullptr;
+  int *counts = nullptr;
+  int64_t cap = 0;
+  hipStream_t side[2] = {nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+};
+static std::mutex g_srbd_scratch_mu;
+static SrbdScratch g_srbd_scratch[64];
+
+static SrbdScratch *srbd_scratch(int64_t batch) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_srbd_scratch_mu);
+  SrbdScratch &s = g_srbd_scratch[dev];
+  if (!s.counts) {
+    if (hipMalloc(&s.counts, 4 * sizeof(int)) != hipSuccess) return nullptr;
+    for (int k = 0; k < 2; ++k) {
+      if (hipStreamCreateWithFlags(&s.side[k], hipStreamNonBlocking) != hipSuccess) return nullptr;
+      if (hipEventCreateWithFlags(&s.join[k], hipEventDisableTiming) != hipSuccess) return nullptr;
+    }
+    if (hipEventCreateWithFlags(&s.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+  }
+  if (batch > s.cap) {
+    if (s.lists) {
+      if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+      (void)hipFree(s.lists);
+      s.lists = nullptr;
+    }
+    const int64_t cap = batch < 4096 ? 4096 : batch;
+    if (hipMalloc(&s.lists, 3 * cap * sizeof(int)) != hipSuccess) {
+      s.cap = 0;
+      return nullptr;
+    }
+    s.cap = cap;
+  }
+  return &s;
+}
+
+// Concurrent class launches (default) or all on the caller's stream
+// (QLOCO_SRBD_FORK=0, comparison runs).
+static bool srbd_fork_enabled() {
+  static const bool on = !(getenv("QLOCO_SRBD_FORK") && atoi(getenv("QLOCO_SRBD_FORK")) == 0);
+  return on;
+}
 
 extern "C" int qloco_srbd_max_stance_vars(void) { return 3 * kBigLegs; }
 
@@ -1566,57 +1767,69 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   a.status = status;
   a.iters = iters;
   a.rho_updates = rho_updates;
-  // Kernel per instance: <= 21 stance legs one-wave workgroups, 22..42
-  // two-wave workgroups, 43..80 the wide kernel (qloco_srbd_big.inc).  When
-  // the batch may hold several classes (the caller's maximum, or 4N when
-  // unknown, says so) it goes through one launch per class on the stream,
-  // each skipping the others' instances after counting its stance legs.  The
-  // last launch takes every instance above the previous classes, so an
-  // instance beyond a too-small caller maximum gets QLOCO_BAD_SIZE there.
+  // Kernel per instance class: <= 21 stance legs one-wave workgroups,
+  // 22..42 two-wave workgroups, 43..80 the wide kernel (qloco_srbd_big.inc).
+  // A batch that may hold several classes (the caller's maximum, or 4N when
+  // unknown, says so) is first classified on the device (srbd_classify_kernel:
+  // one compact instance list per class), then every class kernel walks only
+  // its own list -- no workgroup is spent on another class's instance -- and
+  // the classes run concurrently: class 0 on the caller's stream, classes 1
+  // and 2 on the device's side streams between a fork and a join event, so
+  // one class's tail overlaps another's bulk.  The top class the caller's
+  // maximum admits takes every instance above the lower classes, so an
+  // instance beyond a too-small maximum gets QLOCO_BAD_SIZE there.
   const int legs = max_stance_legs > 0 ? max_stance_legs : 4 * spec->horizon;
   hipStream_t st = (hipStream_t)stream;
   a.leg_lo = 0;
   a.leg_hi = 1 << 30;
   const bool ws = spec->warm_start != 0;
-  auto launch_w1 = [&]() {
-    if (batch <= kSmallBatch) {
+  const dim3 grid((unsigned)batch);
+  auto launch = [&](int cls, hipStream_t s) {
+    if (cls == 0) {
       if (ws)
-        hipLaunchKernelGGL((srbd_admm_kernel<1, 2, true>), dim3((unsigned)batch), dim3(64), 0, st, a);
+        hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, true>), grid, dim3(64), 0, s, a);
       else
-        hipLaunchKernelGGL((srbd_admm_kernel<1, 2, false>), dim3((unsigned)batch), dim3(64), 0, st, a);
+        hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, false>), grid, dim3(64), 0, s, a);
+    } else if (cls == 1) {
+      if (ws)
+        hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, true>), grid, dim3(128), 0, s, a);
+      else
+        hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, false>), grid, dim3(128), 0, s, a);
     } else {
       if (ws)
-        hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, true>),
-                           dim3((unsigned)batch), dim3(64), 0, st, a);
+        hipLaunchKernelGGL((srbd_admm_big_kernel<true>), grid, dim3(kBigThreads), 0, s, a);
       else
-        hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, false>),
-                           dim3((unsigned)batch), dim3(64), 0, st, a);
+        hipLaunchKernelGGL((srbd_admm_big_kernel<false>), grid, dim3(kBigThreads), 0, s, a);
     }
   };
-  if (legs <= kLegsPerWave) {
-    launch_w1();
+  const int top = legs <= kLegsPerWave ? 0 : (legs <= 2 * kLegsPerWave ? 1 : 2);
+  if (top == 0) {
+    launch(0, st);
   } else {
-    a.leg_hi = kLegsPerWave;
-    launch_w1();
-    QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel<1> launch");
-    a.leg_lo = kLegsPerWave + 1;
-    a.leg_hi = legs <= 2 * kLegsPerWave ? (1 << 30) : 2 * kLegsPerWave;
-    if (ws)
-      hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, true>),
-                         dim3((unsigned)batch), dim3(128), 0, st, a);
-    else
-      hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, false>),
-                         dim3((unsigned)batch), dim3(128), 0, st, a);
-    if (legs > 2 * kLegsPerWave) {
-      QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel<2> launch");
-      a.leg_lo = 2 * kLegsPerWave + 1;
-      a.leg_hi = 1 << 30;  // <= 4N = kBigLegs by construction
-      if (ws)
-        hipLaunchKernelGGL((srbd_admm_big_kernel<true>), dim3((unsigned)batch), dim3(kBigThreads),
-                           0, st, a);
-      else
-        hipLaunchKernelGGL((srbd_admm_big_kernel<false>), dim3((unsigned)batch), dim3(kBigThreads),
-                           0, st, a);
+    SrbdScratch *sc = srbd_scratch(batch);
+    if (!sc) return QLOCO_ERR_DEVICE;
+    QLOCO_HIP_CHECK(hipMemsetAsync(sc->counts, 0, 4 * sizeof(int), st), "class counters");
+    hipLaunchKernelGGL(srbd_classify_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st,
+                       a, top, sc->lists, sc->cap, sc->counts);
+    QLOCO_HIP_CHECK(hipGetLastError(), "srbd_classify_kernel launch");
+    const bool fork = srbd_fork_enabled();
+    if (fork) QLOCO_HIP_CHECK(hipEventRecord(sc->fork, st), "fork event");
+    for (int c = 0; c <= top; ++c) {
+      a.list = sc->lists + (int64_t)c * sc->cap;
+      a.count = sc->counts + c;
+      a.leg_lo = 0;
+      a.leg_hi = 1 << 30;
+      hipStream_t s = st;
+      if (fork && c > 0) {
+        s = sc->side[c - 1];
+        QLOCO_HIP_CHECK(hipStreamWaitEvent(s, sc->fork, 0), "fork wait");
+      }
+      launch(c, s);
+      QLOCO_HIP_CHECK(hipGetLastError(), "srbd class kernel launch");
+      if (fork && c > 0) {
+        QLOCO_HIP_CHECK(hipEventRecord(sc->join[c - 1], s), "join event");
+        QLOCO_HIP_CHECK(hipStreamWaitEvent(st, sc->join[c - 1], 0), "join wait");
+      }
     }
   }
   QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel launch");

@@ -66,6 +66,8 @@ class RtNodeBatch:
     def tick(self, gait_msg, ctrl_msg, with_debug=True, stream=None):
         """One loop iteration; gait_msg (B,100), ctrl_msg (B,25) float64 device
         tensors.  Returns (traj, nrt, gen, sched) device tensors (reused)."""
+        _check_rows("gait_msg", gait_msg, (self.batch, GAIT_LEN))
+        _check_rows("ctrl_msg", ctrl_msg, (self.batch, CTRL_LEN))
         _check_rows("gait_msg", gait_msg, (self.batch, GAIT_LEN), self.device)
         _check_rows("ctrl_msg", ctrl_msg, (self.batch, CTRL_LEN), self.device)
         s = _stream(self.ws) if stream is None else stream

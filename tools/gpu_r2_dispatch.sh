@@ -1,0 +1,23 @@
+#!/bin/bash
+# Class dispatch (device classification + per-class lists, concurrent class
+# launches) vs the same with the classes serialised (QLOCO_SRBD_FORK=0) vs
+# the previous full-grid early-exit dispatch (tools/_var/prev), BASELINE
+# configs 3-5 per-GPU shares; plus the GPU parity suite.  Usage: TAG
+set -o pipefail
+tag=${1:-r2d}
+out=gpurun_out/$tag
+mkdir -p $out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { tail -40 $out/pytest_gpu.log; exit 1; }
+tail -n 1 $out/pytest_gpu.log
+for spec in "16 trot 65536" "20 pace 65536" "10 mixed 131072" "10 trot 4096"; do
+  set -- $spec
+  for mode in fork serial prev; do
+    envs=""
+    [ $mode = serial ] && envs="QLOCO_SRBD_FORK=0"
+    [ $mode = prev ] && envs="QLOCO_LIB=tools/_var/prev/libqloco.so"
+    env $envs timeout -k 10 240 python bench.py --horizon $1 --gait $2 --batch $3 --steps 20 --warmup 3 --no-cpu-baseline > $out/b.json 2>> $out/configs.err || { tail -20 $out/configs.err; exit 1; }
+    python -c "import json,sys; d=json.load(open('$out/b.json')); print('%-7s N=%-2s %-6s B=%-7s %8.3f ms/step %10.0f solves/s frac %.3f exec %.3f' % ('$mode', '$1', '$2', '$3', d['ms_per_step'], d['value'], d['roofline']['frac'], d['roofline']['executed_frac']))" >> $out/configs.txt
+  done
+done
+cat $out/configs.txt
