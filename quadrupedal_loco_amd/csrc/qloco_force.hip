@@ -359,3 +359,10 @@ extern "C" int qloco_joint_torques(int64_t batch, const double *Jaco, const int3
   QLOCO_HIP_CHECK(hipGetLastError(), "joint_torque_kernel launch");
   return QLOCO_OK;
 }
+
+#ifdef QLOCO_GI_PHASE_TIMING
+extern "C" int qloco_gi_phase_read(unsigned int *host, size_t count) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(qloco::g_gi_phase), count * sizeof(unsigned int), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif

@@ -45,6 +45,29 @@ struct GiArgs {
 
 #define GI_SYNC() asm volatile("" ::: "memory")
 
+// Development-only phase clocks of the solve (tools/gi_phase.py builds a
+// variant library with -DQLOCO_GI_PHASE_TIMING; the product never defines it)
+#ifdef QLOCO_GI_PHASE_TIMING
+static __device__ unsigned int g_gi_phase[(1 << 16) * 8];
+#define GI_PHASE(i)                                                                   \
+  do {                                                                                \
+    const uint64_t _n = __builtin_readcyclecounter();                                 \
+    const int64_t _g = (int64_t)blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4);  \
+    if (li == 0 && _g < (1 << 16)) g_gi_phase[_g * 8 + (i)] = (unsigned)(_n - _gt0);   \
+  } while (0)
+#define GI_STAMP(v) const uint64_t v = __builtin_readcyclecounter()
+#define GI_ACC(i, v0)                                                                 \
+  do {                                                                                \
+    const uint64_t _n = __builtin_readcyclecounter();                                 \
+    const int64_t _g = (int64_t)blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4);  \
+    if (li == 0 && _g < (1 << 16)) g_gi_phase[_g * 8 + (i)] += (unsigned)(_n - (v0)); \
+  } while (0)
+#else
+#define GI_PHASE(i) ((void)0)
+#define GI_STAMP(v) ((void)0)
+#define GI_ACC(i, v0) ((void)0)
+#endif
+
 __device__ __forceinline__ double gi_distance(double a, double b) {  // EiQuadProg.hpp:100-118
   const double a1 = fabs(a), b1 = fabs(b);
   double t;
@@ -92,21 +115,46 @@ struct GiGroup {
     }
     GI_SYNC();
   }
-  // r(0:iq) = triu(R)^-1 d(0:iq) : serial back substitution (every lane, same order)
+  // r(0:iq) = triu(R)^-1 d(0:iq) : back substitution, every lane the same
+  // operations in the same order, the solved entries carried in registers
+  // (the pass unrolled over the NN possible rows: static register indices),
+  // the R / d reads independent of the chain; lane 0 stores r at the end.
   __device__ __forceinline__ void update_r(int iq) {
-    for (int i = iq - 1; i >= 0; --i) {
+    double rv[NN];
+#pragma unroll
+    for (int i = NN - 1; i >= 0; --i) {
+      rv[i] = 0.0;
+      if (i >= iq) continue;
       double acc = L->d[i];
-      for (int j = i + 1; j < iq; ++j) acc -= L->R[j * NN + i] * L->r[j];
-      GI_SYNC();
-      if (li == 0) L->r[i] = acc / L->R[i * NN + i];
-      GI_SYNC();
+#pragma unroll
+      for (int j = i + 1; j < NN; ++j)
+        if (j < iq) acc -= L->R[j * NN + i] * rv[j];
+      rv[i] = acc / L->R[i * NN + i];
     }
+    GI_SYNC();
+    if (li == 0) {
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+        if (i < iq) L->r[i] = rv[i];
+    }
+    GI_SYNC();
   }
-  // EiQuadProg.cpp:30-93 ; returns false when degenerate
+  // EiQuadProg.cpp:30-93 ; returns false when degenerate.  The Givens sweep
+  // runs on register copies: d (every lane, identical) and this lane's row
+  // of J (lane k: J(k, 0..n-1)); only the stored results go back to LDS.
   __device__ bool add_constraint(int &iq, double &R_norm) {
-    for (int j = n - 1; j >= iq + 1; j--) {
-      double cc = L->d[j - 1];
-      double ss = L->d[j];
+    double dv[NN], jr[NN];
+    const int k = li;
+#pragma unroll
+    for (int c = 0; c < NN; ++c) {
+      dv[c] = L->d[c];
+      jr[c] = (k < n) ? J(k, c) : 0.0;
+    }
+#pragma unroll
+    for (int j = NN - 1; j >= 1; j--) {
+      if (j > n - 1 || j < iq + 1) continue;
+      double cc = dv[j - 1];
+      double ss = dv[j];
       const double h = gi_distance(cc, ss);
       if (h == 0.0) continue;
       ss = ss / h;
@@ -119,22 +167,26 @@ struct GiGroup {
       } else {
         dj1 = h;
       }
-      GI_SYNC();
-      if (li == 0) {
-        L->d[j] = 0.0;
-        L->d[j - 1] = dj1;
-      }
+      dv[j] = 0.0;
+      dv[j - 1] = dj1;
       const double xny = ss / (1.0 + cc);
-      const int k = li;
-      if (k < n) {
-        const double t1 = J(k, j - 1);
-        const double t2 = J(k, j);
-        const double nj1 = t1 * cc + t2 * ss;
-        Jr(k, j - 1) = nj1;
-        Jr(k, j) = xny * (t1 + nj1) - t2;
-      }
-      GI_SYNC();
+      const double t1 = jr[j - 1];
+      const double t2 = jr[j];
+      const double nj1 = t1 * cc + t2 * ss;
+      jr[j - 1] = nj1;
+      jr[j] = xny * (t1 + nj1) - t2;
     }
+    GI_SYNC();
+    if (li == 0) {
+#pragma unroll
+      for (int c = 0; c < NN; ++c) L->d[c] = dv[c];
+    }
+    if (k < n) {
+#pragma unroll
+      for (int c = 0; c < NN; ++c)
+        if (c < n) Jr(k, c) = jr[c];
+    }
+    GI_SYNC();
     iq++;
     if (li < iq) Rr(li, iq - 1) = L->d[li];
     GI_SYNC();
@@ -239,6 +291,13 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
   g.ce0 = ce0;
   g.CI = CI;
   g.ci0 = ci0;
+#ifdef QLOCO_GI_PHASE_TIMING
+  const uint64_t _gt0 = __builtin_readcyclecounter();
+  {
+    const int64_t _g = (int64_t)blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4);
+    if (li == 0 && _g < (1 << 16)) g_gi_phase[_g * 8 + 0] = g_gi_phase[_g * 8 + 6] = g_gi_phase[_g * 8 + 7] = 0;
+  }
+#endif
   const double inf = INFINITY;
   int status = QLOCO_OK;
   int iter = 0;
@@ -288,6 +347,7 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
     if (li == 0) S.R[k * NN + k] = lkk;
     GI_SYNC();
   }
+  GI_PHASE(1);
   if (!pd) {
     status = QLOCO_NOT_PD;
     f_value = inf;
@@ -304,23 +364,39 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
       }
     }
     GI_SYNC();
+    GI_PHASE(2);
     double c2 = 0.0;
     for (int i = 0; i < n; ++i) c2 += S.J[i * NN + i];
-    // x = -G^-1 g0 through the factor (:227-230), serial, lane 0
-    if (li == 0) {
-      for (int i = 0; i < n; ++i) {
+    // x = -G^-1 g0 through the factor (:227-230): every lane the same
+    // forward / back substitution in registers (static indices), lane li
+    // stores x[li]
+    {
+      double xv[NN];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        xv[i] = 0.0;
+        if (i >= n) continue;
         double acc = g0[i];
-        for (int j = 0; j < i; ++j) acc -= S.R[j * NN + i] * S.x[j];
-        S.x[i] = acc / S.R[i * NN + i];
+#pragma unroll
+        for (int j = 0; j < i; ++j) acc -= S.R[j * NN + i] * xv[j];
+        xv[i] = acc / S.R[i * NN + i];
       }
-      for (int i = n - 1; i >= 0; --i) {
-        double acc = S.x[i];
-        for (int j = i + 1; j < n; ++j) acc -= S.R[i * NN + j] * S.x[j];
-        S.x[i] = acc / S.R[i * NN + i];
+#pragma unroll
+      for (int i = NN - 1; i >= 0; --i) {
+        if (i >= n) continue;
+        double acc = xv[i];
+#pragma unroll
+        for (int j = i + 1; j < NN; ++j)
+          if (j < n) acc -= S.R[i * NN + j] * xv[j];
+        xv[i] = acc / S.R[i * NN + i];
       }
-      for (int i = 0; i < n; ++i) S.x[i] = -S.x[i];
+      GI_SYNC();
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+        if (i < n && li == i) S.x[i] = -xv[i];
     }
     GI_SYNC();
+    GI_PHASE(3);
     f_value = 0.0;
     for (int i = 0; i < n; ++i) f_value += g0[i] * S.x[i];
     f_value *= 0.5;
@@ -336,14 +412,22 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
 
     // ---- equality constraints (:237-276), quirks kept
     for (int i = 0; i < me; i++) {
-      bool zero = true;
-      for (int r = 0; r < n; ++r) zero = zero && (g.CEc(r, i) == 0.0);
+      GI_STAMP(_e0);
+      // all n loads in flight at once (no short-circuit chain of loads)
+      bool nz = false;
+#pragma unroll
+      for (int r = 0; r < NN; ++r)
+        if (r < n) nz = nz | (g.CEc(r, i) != 0.0);
+      const bool zero = !nz;
+      GI_ACC(0, _e0);
       if (zero) continue;
+      GI_STAMP(_e1);
       if (li < n) S.np[li] = g.CEc(li, i);
       GI_SYNC();
       g.compute_d();
       g.update_z(iq);
       g.update_r(iq);
+      GI_ACC(6, _e1);
       t2 = 0.0;
       double zz = 0.0, znp = 0.0, npx = 0.0;
       for (int k = 0; k < n; ++k) {
@@ -354,20 +438,25 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
       if (fabs(zz) > DBL_EPSILON) t2 = (-npx - g.ce0[i]) / znp;
       GI_SYNC();
       if (li < n) S.x[li] += t2 * S.z[li];
+      // u(0:iq) -= t2 r(0:iq): independent entries, one per lane
+      for (int k = li; k < iq; k += 16) S.u[k] -= t2 * S.r[k];
       if (li == 0) {
-        for (int k = 0; k < iq; ++k) S.u[k] -= t2 * S.r[k];
         S.u[iq] = t2;
         S.A[i] = -i - 1;
       }
       GI_SYNC();
       f_value += 0.5 * (t2 * t2) * znp;
-      if (!g.add_constraint(iq, R_norm)) {
+      GI_STAMP(_e2);
+      const bool _ok = g.add_constraint(iq, R_norm);
+      GI_ACC(7, _e2);
+      if (!_ok) {
         status = QLOCO_DEGENERATE;
         goto done;
       }
     }
     for (int i = li; i < mi; i += 16) S.iai[i] = i;
     GI_SYNC();
+    GI_PHASE(4);
 
   l1:
     iter++;
@@ -443,8 +532,8 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
       }
       if (t2 >= inf) {
         GI_SYNC();
+        for (int k = li; k < iq; k += 16) S.u[k] -= t * S.r[k];
         if (li == 0) {
-          for (int k = 0; k < iq; ++k) S.u[k] -= t * S.r[k];
           S.u[iq] += t;
           S.iai[l] = l;
         }
@@ -459,10 +548,8 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
       if (li < n) S.x[li] += t * S.z[li];
       f_value += t * znp * (0.5 * t + S.u[iq]);
       GI_SYNC();
-      if (li == 0) {
-        for (int k = 0; k < iq; ++k) S.u[k] -= t * S.r[k];
-        S.u[iq] += t;
-      }
+      for (int k = li; k < iq; k += 16) S.u[k] -= t * S.r[k];
+      if (li == 0) S.u[iq] += t;
       GI_SYNC();
     }
     if (t == t2) {
@@ -518,6 +605,7 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
 
 done:
   GI_SYNC();
+  GI_PHASE(5);
   if (li < n) xout[li] = S.x[li];
   f_out = f_value;
   status_out = status;

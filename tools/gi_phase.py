@@ -1,0 +1,43 @@
+"""Phase clocks of the Goldfarb-Idnani core inside force_qp_kernel
+(development tool).  Needs the variant library built with
+    python tools/variant_lib.py giphase -DQLOCO_GI_PHASE_TIMING=1
+Prints mean cycles per phase: 1 Cholesky, 2 J = L^-T, 3 x0 = -G^-1 g0,
+4 equality constraints, 5 inequality (active-set) loop.
+    QLOCO_LIB=tools/_var/giphase/libqloco.so python tools/gi_phase.py [B]
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+if __name__ == "__main__":
+    import torch
+    from cases import force_inputs
+    from quadrupedal_loco_amd import _lib, qp
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    dev = torch.device("cuda:0")
+    inp = force_inputs(np.random.default_rng(3), B)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in inp.items()}
+    solver = qp.ForceQP(batch=B, device=dev)
+    for _ in range(5):
+        out = solver.step(**d)
+    torch.cuda.synchronize()
+    n = min(B, 1 << 16)
+    buf = np.zeros(n * 8, np.uint32)
+    rc = C.CDLL(_lib.LIB_PATH).qloco_gi_phase_read(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.size))
+    assert rc == 0, rc
+    ph = buf.reshape(-1, 8)[:, :6].astype(np.float64)
+    d = np.diff(ph[:, 1:6], axis=1, prepend=0.0)
+    it = out["iters"].cpu().numpy()
+    print("force QP B=%d  mean active-set iterations %.2f" % (B, it.mean()))
+    for k, lab in enumerate(["Cholesky", "J = L^-T", "x0", "equalities", "inequalities"]):
+        print("  %-13s mean %8.0f  p50 %8.0f  max %8.0f cycles" % (lab, d[:, k].mean(), np.median(d[:, k]), d[:, k].max()))
+    print("  %-13s mean %8.0f cycles" % ("TOTAL", ph[:, 5].mean()))
+    sub = buf.reshape(-1, 8).astype(np.float64)
+    for k, lab in ((0, "eq zero-check"), (6, "eq d/z/r"), (7, "eq add_constr")):
+        print("  %-13s mean %8.0f cycles (sum over the equality loop)" % (lab, sub[:, k].mean()))
