@@ -193,7 +193,7 @@ int qo_force_opt(qo_dyn_state *s, const qo_force_params *prm, const double base_
   int st = QO_OK;
   qo_eqp_solve(s->ws, Gs, g0, CE, ce0, CI, qph, X, &st, iters);
   if (eqp_status) *eqp_status = st;
-  /* QPBaseClass::solveQP: success iff no NaN in X (:200-227) */
+  /* QPBaseClass::solveQP: success iff no NaN in X (go1_rt_control QPBaseClass.cpp:116-142) */
   int ok = 1;
   for (int i = 0; i < 12; ++i)
     if (isnan(X[i])) { ok = 0; break; }

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_
   it = pat;
 #endif
   GI_SYNC();
-  // QPBaseClass::solveQP: success iff no NaN (:200-227); Solve / fallback
+  // QPBaseClass::solveQP: success iff no NaN (go1_rt_control QPBaseClass.cpp:116-142); Solve / fallback
   bool ok = true;
   for (int k = 0; k < 12; ++k) ok = ok && !isnan(P.x[k]);
   if (li < 12) {
