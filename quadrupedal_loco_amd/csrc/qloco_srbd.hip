@@ -99,6 +99,7 @@ struct SrbdLds {
   f4v bv[NC][2];           // per var: {b0,b1,b2,e0}, {e1,e2,step,comp}
   float xs[NC];            // unscaled x per var (P x)
   float Dc[NC];            // Ruiz column scaling D
+#if QLOCO_SRBD_MFMA_INV
   union {
     struct {
       float err[12 * kMaxN];   // per-step row values (gradient error / aggregates)
@@ -109,8 +110,12 @@ struct SrbdLds {
     // k0k2 after every inverse).  W = 1: the transpose buffer (16 x 68);
     // W = 2: per-wave transposes (2 x 16 x 68) or the double-buffered
     // pivot row-block exchange (2 x 8 blocks x 64 lanes x 4)
-    __attribute__((aligned(16))) float sc[QLOCO_SRBD_MFMA_INV ? (W == 1 ? 16 * 68 : 2 * 8 * 256) : 1];
+    __attribute__((aligned(16))) float sc[W == 1 ? 16 * 68 : 2 * 8 * 256];
   };
+#else
+  float err[12 * kMaxN];   // per-step row values (gradient error / aggregates)
+  float Wc[12 * kMaxN];    // per-step Bqp' weights: rows 0..5 W1, rows 6..11 W0
+#endif
   float q2[16];
   float r2[12];
   float x0[16];
@@ -120,6 +125,9 @@ struct SrbdLds {
   float qs[NC];             // per var: scaled q
   int pair[NC];             // per var: 4*step + leg
   int cst[NC];              // per var: step, kMaxN on padding (row of zeros in k0k2)
+#if !QLOCO_SRBD_MFMA_INV
+  f2v k0k2[kMaxN * (kMaxN + 1)];  // [row step][col step]: horizon sums K0, K2
+#endif
   float piv[2];
   float colv[W == 1 ? 1 : 2][W == 1 ? 1 : NC];  // W = 2 inverse: pivot column
   float red[W][16];
@@ -543,6 +551,7 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1>
   bsync<1>();
 }
 
+#if QLOCO_SRBD_MFMA_INV
 // ---- KKT inverse on the matrix cores: block Gauss-Jordan.
 // K (64x64 for W = 1, SPD, padding rows/columns diagonal) is held as blocks
 // of 16x16 in the C/D layout of v_mfma_f32_16x16x4_f32: lane (j, g) =
@@ -767,6 +776,8 @@ __device__ __forceinline__ void invert_w2_mfma(SrbdLds<2> &S, int t, int ncol1, 
   __syncthreads();
 }
 
+#endif  // QLOCO_SRBD_MFMA_INV
+
 // K0 / K2 table over (row step, column step); column kMaxN is the zero row
 // of padding lanes (cst = kMaxN)
 template <int W>
@@ -853,15 +864,19 @@ __device__ unsigned int g_phase[1 << 20];
 #ifndef QLOCO_SRBD_WAVES_PER_EU_W2  // two-wave kernel occupancy
 #define QLOCO_SRBD_WAVES_PER_EU_W2 2
 #endif
-#ifndef QLOCO_SRBD_WAVES_PER_EU  // one-wave kernel occupancy: 3 waves/SIMD
-#define QLOCO_SRBD_WAVES_PER_EU 3    // = 168 VGPRs (small spills in the setup / refactor paths)
+#ifndef QLOCO_SRBD_WAVES_PER_EU  // one-wave kernel occupancy for large batches: 3 waves/SIMD
+#define QLOCO_SRBD_WAVES_PER_EU 3    // = 168 VGPRs (small spills, all in setup / refactor paths)
 #endif
-// With the matrix-core inverse the three-wave kernel is at least as fast as
-// the spill-free two-wave one (194 VGPRs) at every batch size measured
-// (Go1 trot N = 10: B = 1024 / 2048 / 4096 / 8192 143.6 / 214.5 / 286.6 /
-// 465.5 vs 143.4 / 214.9 / 297.8 / 473.2 us; four waves: 137.6 / 207.1 /
-// 290.4 / 510.5; profiles/r2q_persistent_queue_and_occupancy.txt), so it is
-// the only one-wave instantiation.
+// One-wave kernel, small batches (<= kSmallBatch instances, i.e. <= 6 waves
+// per SIMD over the launch): 2 waves/SIMD = 186 VGPRs, spill-free -- with few
+// waves per SIMD the tail of long instances dominates and more registers per
+// wave (no scratch round trips) beat the third resident wave.  Measured on
+// Go1 trot N = 10 (same-call pairs, profiles/r2ab_*, r2v_*): B = 4096 306-307
+// vs 310-314 us, B = 8192 539-555 vs 487-499 us.
+#ifndef QLOCO_SMALL_BATCH
+#define QLOCO_SMALL_BATCH 6144
+#endif
+constexpr int64_t kSmallBatch = QLOCO_SMALL_BATCH;
 #ifndef QLOCO_SRBD_NUM_VGPR_ATTR  // experiments: force a VGPR budget
 #define QLOCO_SRBD_NUM_VGPR_ATTR
 #endif
@@ -1786,10 +1801,17 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   const dim3 grid((unsigned)batch);
   auto launch = [&](int cls, hipStream_t s) {
     if (cls == 0) {
-      if (ws)
-        hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, true>), grid, dim3(64), 0, s, a);
-      else
-        hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, false>), grid, dim3(64), 0, s, a);
+      if (batch <= kSmallBatch) {
+        if (ws)
+          hipLaunchKernelGGL((srbd_admm_kernel<1, 2, true>), grid, dim3(64), 0, s, a);
+        else
+          hipLaunchKernelGGL((srbd_admm_kernel<1, 2, false>), grid, dim3(64), 0, s, a);
+      } else {
+        if (ws)
+          hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, true>), grid, dim3(64), 0, s, a);
+        else
+          hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, false>), grid, dim3(64), 0, s, a);
+      }
     } else if (cls == 1) {
       if (ws)
         hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, true>), grid, dim3(128), 0, s, a);

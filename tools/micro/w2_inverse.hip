@@ -3,7 +3,7 @@
 // matrices with the W = 2 row layout (wave w, lane v: row 64w + v, 128
 // columns; column 63 and columns >= 64 + ncol1 are padding with a diagonal
 // only).  Reports max |K X - I| for each form and condition-number band.
-// Build: hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -mllvm
+// Build: hipcc --offload-arch=gfx950 -O3 -DQLOCO_SRBD_MFMA_INV=1 -fno-slp-vectorize -mllvm
 //   -pragma-unroll-threshold=200000 -I../../include -I../../quadrupedal_loco_amd/csrc
 //   w2_inverse.hip -o w2_inverse
 #include "qloco_srbd.hip"
