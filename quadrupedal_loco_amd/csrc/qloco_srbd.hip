@@ -47,6 +47,9 @@
 #ifndef QLOCO_SRBD_MFMA_INV
 #define QLOCO_SRBD_MFMA_INV 0
 #endif
+#ifndef QLOCO_SRBD_MFMA_W  // which kernels take the matrix-core form: bit 0 W = 1, bit 1 W = 2
+#define QLOCO_SRBD_MFMA_W 3
+#endif
 #ifndef QLOCO_W2_GJ_BUCKETS  // second-half chunk buckets in the W = 2 inverse too
 #define QLOCO_W2_GJ_BUCKETS 0
 #endif
@@ -631,6 +634,64 @@ __device__ __forceinline__ void rowblock_gj(f4v (&Z)[NB], int lane) {
   rowblock_pivot<12, NB, k>(Z, lane); rowblock_pivot<13, NB, k>(Z, lane);
   rowblock_pivot<14, NB, k>(Z, lane); rowblock_pivot<15, NB, k>(Z, lane);
 }
+// In-place 16-pivot GJ of one C-layout block (entry-p trick): the pivot row
+// from lane (j, P/4) register P%4 by ds_bpermute, the pivot column from
+// lane P of each 16-lane row by DPP row_newbcast, the pivot by v_readlane.
+template <int P>
+__device__ __forceinline__ void cblock_pivot(f4v &B, int lane) {
+  constexpr int gq = P >> 2, rq = P & 3;
+  const float prow = f4get(B, rq);
+  const float piv = __builtin_bit_cast(
+      float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, prow), 16 * gq + P));
+  const float pinv = __builtin_amdgcn_rcpf(piv);
+  float e = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(
+                                          4 * (16 * gq + (lane & 15)), __builtin_bit_cast(int, prow)));
+  e = ((lane & 15) == P) ? piv + 1.0f : e;
+  const bool pgrp = (lane >> 4) == gq;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float c = dpp<0x150 + P>(f4get(B, r));  // M[4g + r][P]
+    float g = c * pinv;
+    if (r == rq) g = pgrp ? (1.0f - pinv) : g;
+    f4set(B, r, fmaf(-g, e, f4get(B, r)));
+  }
+}
+__device__ __forceinline__ void cblock_inverse(f4v &B, int lane) {
+  cblock_pivot<0>(B, lane); cblock_pivot<1>(B, lane); cblock_pivot<2>(B, lane);
+  cblock_pivot<3>(B, lane); cblock_pivot<4>(B, lane); cblock_pivot<5>(B, lane);
+  cblock_pivot<6>(B, lane); cblock_pivot<7>(B, lane); cblock_pivot<8>(B, lane);
+  cblock_pivot<9>(B, lane); cblock_pivot<10>(B, lane); cblock_pivot<11>(B, lane);
+  cblock_pivot<12>(B, lane); cblock_pivot<13>(B, lane); cblock_pivot<14>(B, lane);
+  cblock_pivot<15>(B, lane);
+}
+#if QLOCO_SRBD_MFMA_INV == 2
+// Explicit-diagonal form: P = M_kk^-1 by the in-block GJ, T_J = P M_kJ on
+// the matrix cores (A operand the exact transpose of P), then the same
+// Schur / column updates with exact transposes of the old M_Ik.
+template <int k>
+__device__ __forceinline__ void gj_block_step(f4v (&M)[4][4], int lane, const f4v &Id) {
+  cblock_inverse(M[k][k], lane);
+  const f4v P = M[k][k];
+  const f4v Pt = ctrans(P, Id);
+  f4v nT[4];
+#pragma unroll
+  for (int J = 0; J < 4; ++J)
+    if (J != k) nT[J] = -mfma_tn(Pt, M[k][J], (f4v)(0.0f));
+  const f4v nP = -P;
+#pragma unroll
+  for (int I = 0; I < 4; ++I) {
+    if (I == k) continue;
+    const f4v ZI = ctrans(M[I][k], Id);  // old M_Ik^T
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+      if (J != k) M[I][J] = mfma_tn(ZI, nT[J], M[I][J]);
+    M[I][k] = mfma_tn(ZI, nP, (f4v)(0.0f));
+  }
+#pragma unroll
+  for (int J = 0; J < 4; ++J)
+    if (J != k) M[k][J] = -nT[J];
+}
+#else
 template <int k>
 __device__ __forceinline__ void gj_block_step(f4v (&M)[4][4], int lane, const f4v &Id) {
   f4v Z[4];
@@ -652,6 +713,7 @@ __device__ __forceinline__ void gj_block_step(f4v (&M)[4][4], int lane, const f4
 #pragma unroll
   for (int J = 0; J < 4; ++J) M[k][J] = -nT[J];
 }
+#endif
 // Row layout in and out (lane v holds row v of K, then of K^-1) through a
 // transpose buffer tb[c][row] of 16 columns at a time.  The computed K^-1 is
 // not exactly symmetric, so no entry is taken from its mirror (reading
@@ -695,6 +757,39 @@ __device__ __forceinline__ void invert_w1_mfma(SrbdLds<1> &S, int t, int ncol, R
 // block and publishes Z_J = T_J^T through LDS, one barrier, then both waves
 // update their own block rows (each transposes the Z_J it needs); the
 // buffer alternates with k, so a wave may run ahead into step k + 1 safely.
+#if QLOCO_SRBD_MFMA_INV == 2
+template <int k, int w>
+__device__ __forceinline__ void gj2_step(SrbdLds<2> &S, f4v (&M)[4][8], int lane, const f4v &Id) {
+  constexpr int ow = k >> 2, ik = k & 3;
+  f4v *xb = reinterpret_cast<f4v *>(S.sc) + (k & 1) * 8 * 64;  // [block J][lane]: old row block k, P at J = k
+  if constexpr (w == ow) {
+    cblock_inverse(M[ik][k], lane);
+#pragma unroll
+    for (int J = 0; J < 8; ++J) xb[J * 64 + lane] = M[ik][J];
+  }
+  f4v ZI[4];  // old M_Ik^T of this wave's block rows
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (4 * w + i != k) ZI[i] = ctrans(M[i][k], Id);
+  __syncthreads();
+  const f4v P = (w == ow) ? M[ik][k] : xb[k * 64 + lane];
+  const f4v Pt = ctrans(P, Id);
+#pragma unroll
+  for (int J = 0; J < 8; ++J) {
+    if (J == k) continue;
+    const f4v OJ = (w == ow) ? M[ik][J] : xb[J * 64 + lane];
+    const f4v nT = -mfma_tn(Pt, OJ, (f4v)(0.0f));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * w + i != k) M[i][J] = mfma_tn(ZI[i], nT, M[i][J]);
+    if constexpr (w == ow) M[ik][J] = -nT;
+  }
+  const f4v nP = -P;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (4 * w + i != k) M[i][k] = mfma_tn(ZI[i], nP, (f4v)(0.0f));
+}
+#else
 template <int k, int w>
 __device__ __forceinline__ void gj2_step(SrbdLds<2> &S, f4v (&M)[4][8], int lane, const f4v &Id) {
   constexpr int ow = k >> 2, ik = k & 3;
@@ -728,6 +823,7 @@ __device__ __forceinline__ void gj2_step(SrbdLds<2> &S, f4v (&M)[4][8], int lane
     if (4 * w + i != k) M[i][k] = mfma_tn(ZI[i], nP, (f4v)(0.0f));
   if constexpr (w == ow) M[ik][k] = -nP;
 }
+#endif
 template <int w>
 __device__ __forceinline__ void gj2_steps(SrbdLds<2> &S, f4v (&M)[4][8], int lane, int nb) {
   const f4v Id = cident(lane);
@@ -1284,7 +1380,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
       if (first) QL_PHASE(5);
       if constexpr (W == 1) {
         (void)dg;
-#if QLOCO_SRBD_MFMA_INV  // matrix-core block Gauss-Jordan (comparison builds)
+#if QLOCO_SRBD_MFMA_INV && (QLOCO_SRBD_MFMA_W & 1)  // matrix-core block Gauss-Jordan
         invert_w1_mfma(S, t, ncol[0], K);
         fill_k0k2<1>(S, N, Nf, t);  // the staging buffer overlaid the K0 / K2 table
         bsync<1>();
@@ -1301,7 +1397,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
 #endif
       } else {
         (void)dg;
-#if QLOCO_SRBD_MFMA_INV
+#if QLOCO_SRBD_MFMA_INV && (QLOCO_SRBD_MFMA_W & 2)
         invert_w2_mfma(S, t, ncol[1], K);
         fill_k0k2<2>(S, N, Nf, t);
         __syncthreads();
