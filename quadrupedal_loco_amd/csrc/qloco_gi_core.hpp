@@ -204,14 +204,34 @@ struct GiGroup {
         break;
       }
     if (qq < 0) return false;
-    for (int i = qq; i < iq - 1; i++) {
-      GI_SYNC();
-      if (li == 0) {
-        L->A[i] = L->A[i + 1];
-        L->u[i] = L->u[i + 1];
+    // shift A / u / the R columns qq+1..iq-1 one place left: every value
+    // read before any is written (pure moves, the reference's result)
+    {
+      int a_n[2] = {0, 0};
+      double u_n[2] = {0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = qq + li + 16 * q;
+        if (i < iq - 1) {
+          a_n[q] = L->A[i + 1];
+          u_n[q] = L->u[i + 1];
+        }
       }
-      if (li < n) Rr(li, i) = L->R[(i + 1) * NN + li];
+      double rcol[NN];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) rcol[i] = (li < n && i >= qq && i < iq - 1) ? L->R[(i + 1) * NN + li] : 0.0;
       GI_SYNC();
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = qq + li + 16 * q;
+        if (i < iq - 1) {
+          L->A[i] = a_n[q];
+          L->u[i] = u_n[q];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+        if (li < n && i >= qq && i < iq - 1) Rr(li, i) = rcol[i];
     }
     GI_SYNC();
     if (li == 0) {
@@ -461,8 +481,8 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
   l1:
     iter++;
     GI_SYNC();
-    if (li == 0)
-      for (int i = me; i < iq; i++) S.iai[S.A[i]] = -1;
+    // active constraints are distinct indices: one store per lane
+    for (int i = me + li; i < iq; i += 16) S.iai[S.A[i]] = -1;
     GI_SYNC();
     ss = 0.0;
     psi = 0.0;
