@@ -430,48 +430,51 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
     int ip = 0, l = 0;
     double ss = 0.0, psi, t, t1, t2;
 
-    // ---- equality constraints (:237-276), quirks kept
-    for (int i = 0; i < me; i++) {
-      GI_STAMP(_e0);
-      // all n loads in flight at once (no short-circuit chain of loads)
-      bool nz = false;
+    // ---- equality constraints (:237-276), quirks kept.  The reference
+    // skips all-zero CE columns (:239-244); the live columns are found up
+    // front (all loads in flight) and the loop runs over them in column
+    // order, so the four groups of a wave -- whose swing patterns differ --
+    // step through their own live columns together instead of through the
+    // union of everyone's.
+    {
+      unsigned live = 0u;
+      for (int i = 0; i < me; i++) {
+        bool nz = false;
 #pragma unroll
-      for (int r = 0; r < NN; ++r)
-        if (r < n) nz = nz | (g.CEc(r, i) != 0.0);
-      const bool zero = !nz;
-      GI_ACC(0, _e0);
-      if (zero) continue;
-      GI_STAMP(_e1);
-      if (li < n) S.np[li] = g.CEc(li, i);
-      GI_SYNC();
-      g.compute_d();
-      g.update_z(iq);
-      g.update_r(iq);
-      GI_ACC(6, _e1);
-      t2 = 0.0;
-      double zz = 0.0, znp = 0.0, npx = 0.0;
-      for (int k = 0; k < n; ++k) {
-        zz += S.z[k] * S.z[k];
-        znp += S.z[k] * S.np[k];
-        npx += S.np[k] * S.x[k];
+        for (int r = 0; r < NN; ++r)
+          if (r < n) nz = nz | (g.CEc(r, i) != 0.0);
+        if (nz) live |= 1u << i;
       }
-      if (fabs(zz) > DBL_EPSILON) t2 = (-npx - g.ce0[i]) / znp;
-      GI_SYNC();
-      if (li < n) S.x[li] += t2 * S.z[li];
-      // u(0:iq) -= t2 r(0:iq): independent entries, one per lane
-      for (int k = li; k < iq; k += 16) S.u[k] -= t2 * S.r[k];
-      if (li == 0) {
-        S.u[iq] = t2;
-        S.A[i] = -i - 1;
-      }
-      GI_SYNC();
-      f_value += 0.5 * (t2 * t2) * znp;
-      GI_STAMP(_e2);
-      const bool _ok = g.add_constraint(iq, R_norm);
-      GI_ACC(7, _e2);
-      if (!_ok) {
-        status = QLOCO_DEGENERATE;
-        goto done;
+      while (live) {
+        const int i = __builtin_ctz(live);
+        live &= live - 1u;
+        if (li < n) S.np[li] = g.CEc(li, i);
+        GI_SYNC();
+        g.compute_d();
+        g.update_z(iq);
+        g.update_r(iq);
+        t2 = 0.0;
+        double zz = 0.0, znp = 0.0, npx = 0.0;
+        for (int k = 0; k < n; ++k) {
+          zz += S.z[k] * S.z[k];
+          znp += S.z[k] * S.np[k];
+          npx += S.np[k] * S.x[k];
+        }
+        if (fabs(zz) > DBL_EPSILON) t2 = (-npx - g.ce0[i]) / znp;
+        GI_SYNC();
+        if (li < n) S.x[li] += t2 * S.z[li];
+        // u(0:iq) -= t2 r(0:iq): independent entries, one per lane
+        for (int k = li; k < iq; k += 16) S.u[k] -= t2 * S.r[k];
+        if (li == 0) {
+          S.u[iq] = t2;
+          S.A[i] = -i - 1;
+        }
+        GI_SYNC();
+        f_value += 0.5 * (t2 * t2) * znp;
+        if (!g.add_constraint(iq, R_norm)) {
+          status = QLOCO_DEGENERATE;
+          goto done;
+        }
       }
     }
     for (int i = li; i < mi; i += 16) S.iai[i] = i;
@@ -479,6 +482,7 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
     GI_PHASE(4);
 
   l1:
+    GI_STAMP(_i0);
     iter++;
     GI_SYNC();
     // active constraints are distinct indices: one store per lane
@@ -504,6 +508,7 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
     }
     if (li < n) S.xold[li] = S.x[li];
     GI_SYNC();
+    GI_ACC(0, _i0);
 
   l2:
     for (int i = 0; i < mi; i++) {
@@ -522,9 +527,13 @@ __device__ __forceinline__ void gi_solve_group(GiLdsT<NN, MM, PP> &S, int li, in
     GI_SYNC();
 
   l2a:
+    {
+    GI_STAMP(_i1);
     g.compute_d();
     g.update_z(iq);
     g.update_r(iq);
+    GI_ACC(6, _i1);
+    }
     l = 0;
     t1 = inf;
     for (int k = me; k < iq; k++) {

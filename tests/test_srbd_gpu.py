@@ -381,6 +381,32 @@ def test_srbd_config4_share_sampled_against_oracle():
         assert dX <= 0.1 and dF <= 15.0 and dM <= 3.0 and du0 <= 5.0, (b, du0, dF, dM, dX)
 
 
+def test_srbd_config5_share_sampled_against_oracle():
+    """BASELINE configs[4] per-GPU share at full size: mixed trot + bipedal
+    per-instance schedules, N = 10, 131,072 instances in one call (through
+    the device classification and the class lists).  Whole batch: every instance converges, forces finite and inside
+    the friction pyramid; 16 instances spread over the batch against the
+    fp64 restatement with the trajectory-parity bounds above."""
+    N, B = 10, 131072
+    (x0, xr, ft, ct), r = _solve(N, B, "mixed")
+    assert np.all(r["status"] == 0), np.unique(r["status"], return_counts=True)
+    u = r["u"].reshape(B, N, 4, 3)
+    assert np.all(np.isfinite(u))
+    tol = 0.25
+    assert np.all(u[..., 2] >= -tol) and np.all(u[..., 2] <= 180 + tol)
+    assert np.all(np.abs(u[..., 0]) <= 0.3 * u[..., 2] + tol)
+    assert np.all(np.abs(u[..., 1]) <= 0.3 * u[..., 2] + tol)
+    legs = ct.reshape(B, -1).astype(bool).sum(axis=1)
+    assert legs.max() > 21  # the two-wave class, through the device class lists
+    sp = O.srbd_spec(N=N)
+    for b in np.linspace(0, B - 1, 16).astype(int):
+        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
+        xa, info = inst.admm_reduced()
+        assert abs(int(r["iters"][b]) - info.iters) <= 25, (b, r["iters"][b], info.iters)
+        du0, dF, dM, dX = _traj_metrics(r["u"][b], xa, x0[b], xr[b], ft[b], ct[b], N)
+        assert dX <= 0.1 and dF <= 15.0 and dM <= 3.0 and du0 <= 5.0, (b, du0, dF, dM, dX)
+
+
 def test_srbd_persistent_closed_loop_matches_restatement():
     """The reference's member OSQP solver over a control loop
     (A1RobotControl.cpp:556-578: update* + solve with warm start on): 32

@@ -39,5 +39,5 @@ if __name__ == "__main__":
         print("  %-13s mean %8.0f  p50 %8.0f  max %8.0f cycles" % (lab, d[:, k].mean(), np.median(d[:, k]), d[:, k].max()))
     print("  %-13s mean %8.0f cycles" % ("TOTAL", ph[:, 5].mean()))
     sub = buf.reshape(-1, 8).astype(np.float64)
-    for k, lab in ((0, "eq zero-check"), (6, "eq d/z/r"), (7, "eq add_constr")):
-        print("  %-13s mean %8.0f cycles (sum over the equality loop)" % (lab, sub[:, k].mean()))
+    for k, lab in ((0, "ineq l1 (s, psi)"), (6, "ineq l2a d/z/r")):
+        print("  %-16s mean %8.0f cycles (sum over the active-set loop)" % (lab, sub[:, k].mean()))
