@@ -23,6 +23,7 @@ python tools/pmc_summary.py $out/pmc1 srbd_admm > $out/pmc_sq.txt && python tool
 python tools/prof_summary.py traffic $out/fetch $out/write srbd_admm $out/traffic_srbd_n10_b4096.json > /dev/null
 rm -rf $out/pmc1 $out/pmc2 $out/fetch $out/write
 for lib in cur r2start; do
+  [ $lib = r2start ] && [ ! -f tools/_var/r2start/libqloco.so ] && continue
   envs=""
   [ $lib = r2start ] && envs="QLOCO_LIB=tools/_var/r2start/libqloco.so"
   env $envs timeout -k 10 120 python tools/perf_kernel.py default 4096 20 | sed "s/^[a-z0-9]* /$lib /" >> $out/ab_r2start.txt 2>&1 || exit 1
