@@ -11,7 +11,13 @@ instance range is regenerated locally from (seed, global id)) and the solved
 contact forces are all-gathered over RCCL/xGMI inside the timed step.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-                    [--horizon 10] [--gait trot] [--no-cpu-baseline]
+                    [--horizon 10] [--gait trot] [--no-cpu-baseline] [--literal]
+
+The headline solves the stance-only reduction of each QP (swing forces
+eliminated exactly: same optimum).  At N=1 the same line also
+carries `literal_full_qp`: the same workload solved as the reference's
+literal 12N-variable QP (spec.literal_full_qp = 1), timed in
+the same run; `--literal` makes the literal form the headline.
 
 Rank 0 prints ONE JSON line.  Launch for N>1 GPUs:
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -170,6 +176,11 @@ def main():
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--gait", default="trot")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--literal", action="store_true",
+                    help="headline = the reference's literal 12N-variable QP (literal_full_qp = 1)")
+    ap.add_argument("--no-literal-line", action="store_true",
+                    help="skip the literal-QP side measurement at N = 1")
+    ap.add_argument("--literal-steps", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every usable host core)")
@@ -234,8 +245,8 @@ def main():
     d_xr = torch.from_numpy(xr).to(dev)
     d_ft = torch.from_numpy(ft).to(dev)
     d_ct = torch.from_numpy(ct).to(dev)
-    solver = srbd.BatchedConvexMpc(horizon=N)
-    legs = srbd.max_stance_legs(ct, N)
+    solver = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=int(args.literal))
+    legs = 4 * N if args.literal else srbd.max_stance_legs(ct, N)
     gather = None
     multi = world > 1 or args.force_dist
     overlap = multi and not args.no_allgather and args.overlap
@@ -307,7 +318,7 @@ def main():
     status = out.status.cpu().numpy()
     iters = out.iters.cpu().numpy()
     rho_up = out.rho_updates.cpu().numpy()
-    n_var = 3 * ct.reshape(B, -1).sum(axis=1)
+    n_var = 12 * N * np.ones(B) if args.literal else 3 * ct.reshape(B, -1).sum(axis=1)
     checks = iters // 25 + iters // 100
     flops_alg = float(srbd_flops_alg(N, iters, rho_up).sum())
     flops_exec = float(srbd_flops_executed(n_var, iters, rho_up, N, checks).sum())
@@ -332,7 +343,9 @@ def main():
             "workload": "Go1 %s convex MPC N=%d fp32, batch=%d per GPU%s"
                         % (args.gait, N, B, _config_tag(N, args.gait, B)),
             "horizon": N, "batch_per_gpu": B, "gait": args.gait,
-            "solver": "OSQP-algorithm ADMM, default settings (eps 1e-3, adaptive rho)",
+            "solver": "OSQP-algorithm ADMM, default settings (eps 1e-3, adaptive rho), %s" % (
+                "literal 12N-variable QP (literal_full_qp=1)" if args.literal else
+                "stance-only reduction of the 12N-variable QP (same optimum)"),
             "parallelism": "dp%d (%s instance shards, RCCL all-gather of u0%s)" % (
                 world, shard, ", overlapped with the next solve" if overlap else ""),
         },
@@ -344,7 +357,7 @@ def main():
         "admm_iters_p50_p99": [int(np.percentile(iters, 50)), int(np.percentile(iters, 99))],
         "status_ok_frac": float(np.mean(status == 0)),
         "roofline": {
-            "bound": "mfma",
+            "bound": "valu-fp32",
             "achieved": round(achieved_tflops, 3),
             "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
@@ -353,11 +366,14 @@ def main():
             "algorithmic_flops_per_launch": flops_alg,
             "executed": round(executed_tflops, 3),
             "executed_frac": round(executed_tflops / PEAK_FP32_TFLOPS, 4),
-            "note": "FP32 compute bound (VALU; FP32 vector peak == FP32 MFMA peak 157.3 TF). "
-                    "achieved = SURVEY.md 8(d) algorithmic flops of the reference's 12N-variable "
-                    "QP (%.3g per launch) / mean kernel time (HIP events on the launch stream); "
-                    "executed = flops this kernel actually performs on the stance-only QP "
-                    "(%.3g per launch), DESIGN.md 5" % (flops_alg, flops_exec),
+            "note": ("FP32 VALU compute bound: no MFMA instruction runs on this path (the "
+                     "closed-form Hessian removes the B'QB GEMM, DESIGN.md 3); peak = FP32 vector "
+                     "157.3 TF.  achieved / frac count SURVEY.md 8(d)'s ALGORITHMIC flops of the "
+                     "reference's 12N-variable QP (%.3g per launch) / mean kernel time (HIP events "
+                     "on the launch stream)%s; executed / executed_frac = the flops this kernel "
+                     "actually performs (%.3g per launch, DESIGN.md 5) -- the number that rates "
+                     "the kernel" % (flops_alg, "" if args.literal else
+                                     ", which the stance-only kernel never builds", flops_exec)),
         },
     }
     tfile = os.path.join(ROOT, "profiles", "traffic_srbd_n%d_b%d.json" % (N, B))
@@ -365,12 +381,54 @@ def main():
         with open(tfile) as f:
             res["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
 
+    if rank == 0 and world == 1 and not args.literal and not args.no_literal_line:
+        res["literal_full_qp"] = literal_line(args, srbd, d_x0, d_xr, d_ft, d_ct, stream, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(N, args.gait, args.cpu_seconds, args.cpu_threads)
     if rank == 0:
         print(json.dumps(res), file=json_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def literal_line(args, srbd, d_x0, d_xr, d_ft, d_ct, stream, dev):
+    """The same workload solved as the reference's literal 12N-variable QP
+    (literal_full_qp = 1: swing forces kept as ADMM variables), timed after the
+    headline loop: barrier-free single-GPU timing, HIP events per launch."""
+    import torch
+    B, N, K = args.batch, args.horizon, args.literal_steps
+    solver = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=1)
+    out = solver.alloc_outputs(B, dev)
+    for _ in range(5):
+        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, stream=stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1)]
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for i in range(K):
+        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, stream=stream.cuda_stream)
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    per = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(K)])
+    iters = out.iters.cpu().numpy()
+    rho_up = out.rho_updates.cpu().numpy()
+    status = out.status.cpu().numpy()
+    checks = iters // 25 + iters // 100
+    fa = float(srbd_flops_alg(N, iters, rho_up).sum())
+    fe = float(srbd_flops_executed(12 * N * np.ones(B), iters, rho_up, N, checks).sum())
+    kt = float(per.mean()) * 1e-3
+    return {"value": round(B * K / elapsed, 1), "unit": "solves/s", "steps": K,
+            "ms_per_step": round(elapsed / K * 1e3, 4),
+            "kernel_us_avg": round(float(per.mean()) * 1e3, 2),
+            "p99_batch_us": round(float(np.percentile(per, 99)) * 1e3, 2),
+            "admm_iters_p50_p99": [int(np.percentile(iters, 50)), int(np.percentile(iters, 99))],
+            "status_ok_frac": float(np.mean(status == 0)),
+            "frac": round(fa / kt / 1e12 / PEAK_FP32_TFLOPS, 4),
+            "executed_frac": round(fe / kt / 1e12 / PEAK_FP32_TFLOPS, 4),
+            "note": "the reference's call as written (A1RobotControl.cpp:557-578): all 12N "
+                    "forces ADMM variables, swing legs held by fz in [0, 0] equality rows; "
+                    "120 variables per N = 10 instance -> two-wavefront workgroups"}
 
 
 def cpu_baseline(N, gait, seconds, threads):

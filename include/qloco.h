@@ -85,7 +85,15 @@ typedef struct qloco_srbd_spec {
                              /*    before the first call; see DESIGN.md §3          */
   int32_t polish;            /* must be 0: OSQP polishing is not implemented (the    */
                              /* reference leaves it off); 1 -> QLOCO_ERR_ARG         */
-  int32_t reserved[6];
+  int32_t literal_full_qp;   /* 0: the stance-only reduction (swing forces removed  */
+                             /*    exactly; same optimum, fastest kernels)          */
+                             /* 1: the reference's call as written: all 12N forces  */
+                             /*    are ADMM variables, swing legs held by their     */
+                             /*    fz in [fz_min*c, fz_max*c] = [0, 0] rows (OSQP   */
+                             /*    equality rows, rho_eq = 1e3 rho), Ruiz over the  */
+                             /*    full P and A (ConvexMpc.cpp:162-264,             */
+                             /*    A1RobotControl.cpp:557-578); DESIGN.md §3e       */
+  int32_t reserved[5];
 } qloco_srbd_spec;
 
 /* Per-instance record of the persistent solver (spec.warm_start == 2),
@@ -93,10 +101,17 @@ typedef struct qloco_srbd_spec {
  *   [0,12N) scaled x  [12N,32N) scaled z  [32N,52N) scaled y
  *   [52N,64N) unscaled x  [64N,84N) unscaled y  [84N,96N) unscaled q
  *   [96N,100N) contact flags  [100N] rho  [100N+1] 1 after the first call.
- * Same stance set as the last call: OSQP's update path (osqp_update_P /
- * _lin_cost / _bounds + solve: Ruiz on the new P with the previous q in the
- * cost scale, adapted rho kept, scaled iterates carried); a changed stance
- * set re-initialises (settings rho) warm-started from the last solution. */
+ * literal_full_qp = 1 (the reference's semantics): the first call sets the
+ * solver up, EVERY later call takes OSQP's update path (osqp_update_P /
+ * _lin_cost / _lower_bound / _upper_bound + solve: Ruiz on the new P with
+ * the previous q in the cost scale, the rho vector re-typed from the new
+ * bounds, the adapted rho kept, the scaled x, z, y carried) -- the
+ * reference's Hessian pattern does not depend on the contacts, so OsqpEigen
+ * never re-initialises.  literal_full_qp = 0 (stance-only reduction, whose
+ * variable set follows the stance set): same stance set as the last call ->
+ * the update path; a changed stance set re-initialises (settings rho),
+ * warm-started from the last unscaled solution -- a documented deviation
+ * from the reference. */
 #define QLOCO_SRBD_PERSIST_LEN(N) (100 * (N) + 4)
 
 /* Go1 SRBD constants + OSQP default settings. */
@@ -162,7 +177,11 @@ int qloco_gen_srbd_host_strided(uint64_t seed, int32_t horizon, float dt, int32_
 /*    replaces QPsolver_EiQuadProg::solve -> Eigen::QP::solve_quadprog      */
 /*    (rt_mpc_qp/src/QP/QPBaseClass.cpp:36-58; EiQuadProg.cpp:172-513),     */
 /*    quirk-compatible.  Double precision.              */
-/*    n <= 16, p <= 16, m <= 64.  Matrices col-major, per instance:         */
+/*    n <= 64, p <= 64, m <= 320 (covers QPBaseClass's nVars <= 60,         */
+/*    nIneq <= 300, QPBaseClass.h:49-51): n, p <= 16 and m <= 64 run four   */
+/*    QPs per wavefront (bit-exact with the restatement in the common       */
+/*    case), larger ones one per wavefront (to rounding; qloco_gi_wide.hip). */
+/*    Matrices col-major, per instance:                                      */
 /*    G[n*n] (only the lower triangle is read), g0[n], CE[n*p], ce0[p],     */
 /*    CI[n*m], ci0[m].  A NULL CE/ce0/CI/ci0 with stride 0 broadcasts one    */
 /*    shared copy; *_stride = elements between instances (0 = shared).     */
@@ -176,6 +195,8 @@ int qloco_eiquadprog_solve(int32_t n, int32_t p, int32_t m, int64_t batch, const
                            const double *ci0, int64_t ci0_stride, double *x, double *f,
                            int32_t *status, int32_t *iters, void *stream);
 int qloco_max_gi_vars(void);
+/* the size limits above: n, p, m (any pointer may be NULL) */
+void qloco_gi_limits(int32_t *n, int32_t *p, int32_t *m);
 
 /* ====================================================================== */
 /* 3. Go1 force-distribution QP, batched                                    */

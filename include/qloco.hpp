@@ -190,8 +190,12 @@ class PRMPCClass {
 // Like the reference's member OsqpEigen::Solver (A1RobotControl.h:67, set up
 // once with warm start on, then update* + solve every tick, :556-578), each
 // robot's solver persists across compute_grf calls (spec.warm_start = 2, the
-// per-robot record on the device); reset() forgets it.  Pass a spec with
-// warm_start = 0 for independent cold solves.
+// per-robot record on the device) and, by default, solves the reference's
+// literal 12N-variable QP (spec.literal_full_qp = 1), so every call after
+// the first takes OSQP's update path as the reference's does, contact
+// changes included; reset() forgets it.  Pass a spec with warm_start = 0
+// for independent cold solves, literal_full_qp = 0 for the faster
+// stance-only reduction (same optimum; DESIGN.md §3c for its persistence).
 struct A1MpcState {                // the A1CtrlStates fields compute_grf reads
   double root_euler[3], root_pos[3], root_ang_vel[3], root_lin_vel[3];
   double root_rot_mat[9];          // col-major; used for root_lin_vel_d_world
@@ -209,11 +213,16 @@ class ConvexMpcBatch {
   void solve_device(const float *x0, const float *x_ref, const float *feet,
                     const uint8_t *contacts, float *u0, int32_t *status, int32_t *iters);
   void reset();  // fresh solvers (the next call sets each one up again)
+  // settings / weights may be edited between calls; horizon and warm_start
+  // size the device buffers and are fixed at construction (a changed value
+  // throws qloco::Error on the next call)
   qloco_srbd_spec spec;
   std::vector<int32_t> status, iters;
 
  private:
+  void check_spec() const;
   int batch_;
+  int horizon_ = 0, warm_mode_ = 0;
   DeviceArena arena_;
   float *d_x0_, *d_xr_, *d_feet_, *d_u0_, *d_rec_ = nullptr;
   uint8_t *d_ct_;

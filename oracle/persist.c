@@ -15,14 +15,19 @@
  *   osqp_update_*_bound    l, u = E l_new, E u_new; update_rho_vec
  *   osqp_solve         no cold start: the scaled x, z, y of the last solve
  *                      as they are; rho as adapted by the last solve
- * The GPU kernel solves the stance-only reduction of the QP,
- * whose dimensions change with the stance set.  Same stance set as the last
- * call: the update path above (QO_ADMM_RESUME).  Changed stance set: the
- * analogue of OsqpEigen's re-initialisation branch for a changed problem
- * structure (getPrimal/DualVariable, clearSolver, initSolver, setPrimal/
- * DualVariable): fresh setup (settings rho) warm-started from the last
- * unscaled solution (QO_ADMM_WARM), variables / rows that were not stance
- * starting at 0.  First call: cold.
+ The literal 12N-variable QP (literal = 1, the reference's call): the
+ * Hessian pattern does not depend on the contacts, so every call after the
+ * first is the update path above; the new bounds re-type the fz rows whose
+ * contact flag changed (update_rho_vec: l == u -> equality, 1e3 rho), which
+ * set_rho_vec inside qo_admm_solve_ex does from the new bounds.
+ * The stance-only reduction (literal = 0, the fast kernels' problem, DESIGN.md
+ * §3) changes dimensions with the stance set.  Same stance set as the last
+ * call: the update path (QO_ADMM_RESUME).  Changed stance set: the analogue
+ * of OsqpEigen's re-initialisation branch for a changed problem structure
+ * (getPrimal/DualVariable, clearSolver, initSolver, setPrimal/DualVariable):
+ * fresh setup (settings rho) warm-started from the last unscaled solution
+ * (QO_ADMM_WARM), variables / rows that were not stance starting at 0 -- a
+ * documented deviation from the reference.  First call: cold.
  *
  * Record layout (doubles, full index: variable 12k + 3i + c, row 20k + 5i + r):
  *   [0,12N) xs   [12N,32N) zs   [32N,52N) ys      scaled iterates
@@ -39,6 +44,14 @@ int qo_srbd_persist_step(double *rec, const qo_srbd_spec *sp, const qo_admm_sett
                          const float *x0f, const float *xrf, const float *ftf, int feet_per_step,
                          const uint8_t *contacts, int contacts_per_step, double *u,
                          qo_admm_info *info) {
+  return qo_srbd_persist_step_ex(rec, sp, st, x0f, xrf, ftf, feet_per_step, contacts,
+                                 contacts_per_step, 0, u, info);
+}
+
+int qo_srbd_persist_step_ex(double *rec, const qo_srbd_spec *sp, const qo_admm_settings *st,
+                            const float *x0f, const float *xrf, const float *ftf,
+                            int feet_per_step, const uint8_t *contacts, int contacts_per_step,
+                            int literal, double *u, qo_admm_info *info) {
   const int N = sp->N, nu = 12 * N, nc = 20 * N;
   double *xs = rec, *zs = rec + 12 * N, *ys = rec + 32 * N, *xu = rec + 52 * N;
   double *yu = rec + 64 * N, *qp = rec + 84 * N, *ct = rec + 96 * N;
@@ -57,11 +70,12 @@ int qo_srbd_persist_step(double *rec, const qo_srbd_spec *sp, const qo_admm_sett
   double *C = (double *)malloc(sizeof(double) * nc * nu);
   qo_srbd_build_instance(sp, x0, xr, ft, feet_per_step, c, 1, H, g, lb, ub);
   qo_srbd_constraints(sp, C);
-  /* stance reduction: variables and rows of stance (step, leg) pairs */
+  /* stance reduction: variables and rows of stance (step, leg) pairs;
+   * the literal QP keeps every pair (ConvexMpc.cpp:227-249, A1RobotControl.cpp:560-567) */
   int *vi = (int *)malloc(sizeof(int) * nu), *ri = (int *)malloc(sizeof(int) * nc);
   int n = 0, m = 0;
   for (int k = 0; k < 4 * N; ++k)
-    if (c[k]) {
+    if (literal || c[k]) {
       for (int j = 0; j < 3; ++j) vi[n++] = 3 * k + j;
       for (int j = 0; j < 5; ++j) ri[m++] = 5 * k + j;
     }
@@ -80,7 +94,11 @@ int qo_srbd_persist_step(double *rec, const qo_srbd_spec *sp, const qo_admm_sett
     uu[r] = ub[ri[r]];
   }
   int same = *calls > 0.0;
-  for (int k = 0; k < 4 * N && same; ++k) same = (ct[k] != 0.0) == (c[k] != 0);
+  /* the literal problem's structure never changes: after the first call every
+   * call is OsqpEigen's update path (updateHessianMatrix finds the pattern of
+   * hessian = dense_hessian.sparseView() unchanged, ConvexMpc.cpp:211-215) */
+  if (!literal)
+    for (int k = 0; k < 4 * N && same; ++k) same = (ct[k] != 0.0) == (c[k] != 0);
   double *ix = (double *)calloc(n ? n : 1, sizeof(double)), *iz = (double *)calloc(m ? m : 1, sizeof(double));
   double *iy = (double *)calloc(m ? m : 1, sizeof(double)), *iq = (double *)calloc(n ? n : 1, sizeof(double));
   qo_admm_init in;

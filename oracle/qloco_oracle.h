@@ -296,6 +296,20 @@ int qo_srbd_persist_step(double *rec, const qo_srbd_spec *sp, const qo_admm_sett
                          const float *x0, const float *x_ref, const float *feet,
                          int feet_per_step, const uint8_t *contacts, int contacts_per_step,
                          double *u, qo_admm_info *info);
+/* literal = 1: the reference's semantics on its literal 12N-variable QP
+ * (every (step, leg) pair a variable, swing pairs held by fz in [0, 0]):
+ * the first call is a cold setup, EVERY later call takes QO_ADMM_RESUME --
+ * OsqpEigen's updateHessianMatrix finds the (contact-independent, dense)
+ * Hessian pattern unchanged and calls osqp_update_P, then
+ * osqp_update_lin_cost and osqp_update_{lower,upper}_bound, whose
+ * update_rho_vec re-types the fz rows whose contact flag changed
+ * (equality <-> inequality, rho_vec from the adapted rho); osqp_solve then
+ * starts from the scaled x, z, y of the last solve.  literal = 0: as
+ * qo_srbd_persist_step. */
+int qo_srbd_persist_step_ex(double *rec, const qo_srbd_spec *sp, const qo_admm_settings *st,
+                            const float *x0, const float *x_ref, const float *feet,
+                            int feet_per_step, const uint8_t *contacts, int contacts_per_step,
+                            int literal, double *u, qo_admm_info *info);
 
 /* Exact optimum of the same box/row-bounded QP via the EiQuadProg
  * restatement (p = 0, so none of the equality quirks apply).             */

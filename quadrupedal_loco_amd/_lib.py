@@ -28,7 +28,7 @@ class SrbdSpec(C.Structure):
         ("max_iter", C.c_int32), ("check_termination", C.c_int32), ("scaling", C.c_int32),
         ("adaptive_rho", C.c_int32), ("adaptive_rho_interval", C.c_int32),
         ("adaptive_rho_tolerance", C.c_float), ("warm_start", C.c_int32),
-        ("polish", C.c_int32), ("reserved", C.c_int32 * 6),
+        ("polish", C.c_int32), ("literal_full_qp", C.c_int32), ("reserved", C.c_int32 * 5),
     ]
 
 
@@ -75,6 +75,7 @@ SIGNATURES = {
     "qloco_eiquadprog_solve": (C.c_int, [i32, i32, i32, i64, vp, i64, vp, i64, vp, i64, vp, i64,
                                          vp, i64, vp, i64, vp, vp, vp, vp, vp]),
     "qloco_max_gi_vars": (C.c_int, []),
+    "qloco_gi_limits": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "qloco_force_params_default": (None, [C.POINTER(ForceParams)]),
     "qloco_force_qp_solve": (C.c_int, [C.POINTER(ForceParams), i64] + [vp] * 18),
     "qloco_leg_fk": (C.c_int, [i64] + [vp] * 7),

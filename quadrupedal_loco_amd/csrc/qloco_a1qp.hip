@@ -21,9 +21,14 @@
 // complete in order, so wave-level fences replace barriers.
 //
 // fp64 throughout, compiled without FMA contraction and with the oracle's
-// (oracle/a1_qp.c, oracle/admm.c) summation orders, so the build is
-// bit-identical to the restatement; the linear solve uses the explicit
-// Gauss-Jordan inverse instead of the oracle's Cholesky solves.
+// (oracle/a1_qp.c, oracle/admm.c) summation orders, so the QP BUILD (H, g, A,
+// l, u) is bit-identical to the restatement.  The ADMM is not: the linear
+// solve uses an explicit Gauss-Jordan inverse where the oracle uses Cholesky
+// solves, so iterates differ by rounding (tests/test_a1qp_gpu.py allows
+// 1e-7 relative / 0.5 N and iteration counts within one check interval).
+// The fixture tests/golden/a1_qp.npz comes from the repo's own restatement
+// (make_a1_golden.py): parity with the reference's OsqpEigen solve is
+// unpinned (OSQP is not vendored).
 #include <math.h>
 #include <string.h>
 

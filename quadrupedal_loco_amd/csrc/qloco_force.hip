@@ -49,18 +49,23 @@ struct ForceLds {
 
 __device__ __forceinline__ double sq(double v) { return v * v; }
 
-// dynmics_compute.cpp:141-261 (scalar, executed redundantly by the group)
-__device__ void force_distribution(const double *com_des, const double *leg_des,
-                                   const double *F, int mode, double y_coefficient,
-                                   const double *rfoot_des, const double *lfoot_des,
-                                   double *R /* F_leg_ref 3x4 col-major, in/out */) {
-#define FRC(r, c) R[(c)*3 + (r)]
-  const double body_FR_dis = sqrt(sq(com_des[0] - leg_des[0]) + sq(com_des[1] - leg_des[1]) + sq(com_des[2] - leg_des[2]));
-  const double body_FL_dis = sqrt(sq(com_des[0] - leg_des[3]) + sq(com_des[1] - leg_des[4]) + sq(com_des[2] - leg_des[5]));
-  const double body_RR_dis = sqrt(sq(com_des[0] - leg_des[6]) + sq(com_des[1] - leg_des[7]) + sq(com_des[2] - leg_des[8]));
-  const double body_RL_dis = sqrt(sq(com_des[0] - leg_des[9]) + sq(com_des[1] - leg_des[10]) + sq(com_des[2] - leg_des[11]));
-  double f_double;
-  if (mode == 101) {
+// dynmics_compute.cpp:141-261 (scalar, executed redundantly by the group).
+// Both gait branches are evaluated and the result selected per entry: with
+// per-branch stores the compiler sinks them into one dynamically indexed
+// store and R lands in scratch (a per-lane spill written back to HBM).
+__device__ __forceinline__ void force_distribution(const double *com_des, const double *leg_des,
+                                                   const double *F, int mode, double y_coefficient,
+                                                   const double *rfoot_des, const double *lfoot_des,
+                                                   double (&R)[12] /* F_leg_ref 3x4 col-major, in/out */) {
+  // mode 101 (:155-182): distance ratios
+  double p1[12];
+#define FRC(r, c) p1[(c)*3 + (r)]
+  {
+    const double body_FR_dis = sqrt(sq(com_des[0] - leg_des[0]) + sq(com_des[1] - leg_des[1]) + sq(com_des[2] - leg_des[2]));
+    const double body_FL_dis = sqrt(sq(com_des[0] - leg_des[3]) + sq(com_des[1] - leg_des[4]) + sq(com_des[2] - leg_des[5]));
+    const double body_RR_dis = sqrt(sq(com_des[0] - leg_des[6]) + sq(com_des[1] - leg_des[7]) + sq(com_des[2] - leg_des[8]));
+    const double body_RL_dis = sqrt(sq(com_des[0] - leg_des[9]) + sq(com_des[1] - leg_des[10]) + sq(com_des[2] - leg_des[11]));
+    double f_double;
     f_double = F[0] * body_FL_dis / (body_FL_dis + body_RL_dis);
     FRC(0, 3) = f_double;
     FRC(0, 1) = F[0] - f_double;
@@ -79,7 +84,13 @@ __device__ void force_distribution(const double *com_des, const double *leg_des,
     f_double = F[5] * body_FR_dis / (body_FR_dis + body_RR_dis);
     FRC(2, 2) = f_double;
     FRC(2, 0) = F[5] - f_double;
-  } else if (mode == 102) {
+  }
+#undef FRC
+  // mode 102 (:185-246): projection ratios clamped to [0, 1]
+  double p2[12];
+#define FRC(r, c) p2[(c)*3 + (r)]
+  {
+    double f_double;
     const double v0 = leg_des[9] - leg_des[0], v1 = leg_des[10] - leg_des[1], v2 = leg_des[11] - leg_des[2];
     const double c0 = lfoot_des[0] - leg_des[0], c1 = lfoot_des[1] - leg_des[1], c2 = lfoot_des[2] - leg_des[2];
     const double rlleg_dis = sqrt(sq(v0) + sq(v1) + sq(v2));
@@ -112,8 +123,11 @@ __device__ void force_distribution(const double *com_des, const double *leg_des,
     f_double = F[5] * rleg_comx;
     FRC(2, 2) = f_double;
     FRC(2, 1) = F[5] - f_double;
-  }  // other modes: F_leg_ref unchanged (:247-250)
+  }
 #undef FRC
+  // other modes: F_leg_ref unchanged (:247-250)
+#pragma unroll
+  for (int k = 0; k < 12; ++k) R[k] = mode == 101 ? p1[k] : (mode == 102 ? p2[k] : R[k]);
 }
 
 #ifndef QLOCO_FORCE_WPE  // waves per SIMD the register budget targets
@@ -160,7 +174,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_
   force_distribution(a.com_des + inst * 3, a.leg_des + inst * 12, a.F_force_des + inst * 6,
                      a.mode[inst], a.y_coef[inst], a.rfoot_des + inst * 3, a.lfoot_des + inst * 3,
                      Fref);
-  if (li < 12) P.guess[li] = Fref[li];
+  // this lane's entry by a static select chain: indexing Fref by li would put
+  // the array in scratch (a per-lane spill of 96 B, written back to HBM)
+  {
+    double mine = Fref[0];
+#pragma unroll
+    for (int k = 1; k < 12; ++k) mine = (li == k) ? Fref[k] : mine;
+    if (li < 12) P.guess[li] = mine;
+  }
   // ---- force_opt: A (6x12, col-major) with the skew_hat quirk (:274-298)
   if (li < 12) {
     for (int k = 0; k < 6; ++k) PA[li * 6 + k] = 0.0;

@@ -14,7 +14,7 @@
 // -ffp-contract=off, and every dot product is summed by ONE lane in the
 // reference's index order, so the arithmetic is the restatement's
 // (oracle/eiquadprog.c) operation for operation -- active-set decisions and
-// results agree bit for bit in the common case (tests/test_gi_gpu.py).
+// results agree bit for bit in the common case (tests/test_qp_gpu.py).
 //
 // The index quirks of the reference are kept: me = p
 // counts skipped zero CE columns, equality markers are stored at A(i), the
@@ -24,6 +24,7 @@
 #include <string.h>
 
 #include "qloco_gi_core.hpp"
+#include "qloco_gi_wide.hpp"
 
 namespace qloco {
 
@@ -51,7 +52,13 @@ __global__ __launch_bounds__(64) void gi_kernel(const GiArgs a) {
 
 using namespace qloco;
 
-extern "C" int qloco_max_gi_vars(void) { return GI_N; }
+extern "C" int qloco_max_gi_vars(void) { return kGiWideN; }
+
+extern "C" void qloco_gi_limits(int32_t *n, int32_t *p, int32_t *m) {
+  if (n) *n = kGiWideN;
+  if (p) *p = kGiWideP;
+  if (m) *m = kGiWideM;
+}
 
 extern "C" int qloco_eiquadprog_solve(int32_t n, int32_t p, int32_t m, int64_t batch,
                                       const double *G, int64_t G_stride, const double *g0,
@@ -60,10 +67,18 @@ extern "C" int qloco_eiquadprog_solve(int32_t n, int32_t p, int32_t m, int64_t b
                                       int64_t CI_stride, const double *ci0, int64_t ci0_stride,
                                       double *x, double *f, int32_t *status, int32_t *iters,
                                       void *stream) {
-  if (n < 1 || n > GI_N || p < 0 || p > GI_P || m < 0 || m > GI_M) return QLOCO_BAD_SIZE;
+  if (n < 1 || n > kGiWideN || p < 0 || p > kGiWideP || m < 0 || m > kGiWideM)
+    return QLOCO_BAD_SIZE;
   if (batch < 0 || !G || !g0 || !x) return QLOCO_ERR_ARG;
   if ((p > 0 && (!CE || !ce0)) || (m > 0 && (!CI || !ci0))) return QLOCO_ERR_ARG;
   if (batch == 0) return QLOCO_OK;
+  // the small QPs of the hot path (force QP 12/12/24, body QP 8/0/48): four
+  // per wavefront; anything larger up to QPBaseClass's capacity: one per
+  // wavefront (qloco_gi_wide.hip)
+  if (n > GI_N || p > GI_P || m > GI_M)
+    return gi_wide_launch(n, p, m, batch, G, G_stride, g0, g0_stride, CE, CE_stride, ce0,
+                          ce0_stride, CI, CI_stride, ci0, ci0_stride, x, f, status, iters,
+                          (hipStream_t)stream);
   GiArgs a;
   memset(&a, 0, sizeof(a));
   a.n = n;

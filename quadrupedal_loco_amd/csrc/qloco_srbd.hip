@@ -34,25 +34,20 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
+#include <utility>
+#include <vector>
 
 #include <type_traits>
 
 #include "qloco_common.hpp"
 #include "qloco_dpp.inc"
 
-// The KKT inverse: register-row DPP Gauss-Jordan (default) or the
-// matrix-core block Gauss-Jordan (QLOCO_SRBD_MFMA_INV=1; as accurate, but
-// slower once made stable -- measured).
-#ifndef QLOCO_SRBD_MFMA_INV
-#define QLOCO_SRBD_MFMA_INV 0
-#endif
-#ifndef QLOCO_SRBD_MFMA_W  // which kernels take the matrix-core form: bit 0 W = 1, bit 1 W = 2
-#define QLOCO_SRBD_MFMA_W 3
-#endif
-#ifndef QLOCO_W2_GJ_BUCKETS  // second-half chunk buckets in the W = 2 inverse too
-#define QLOCO_W2_GJ_BUCKETS 0
-#endif
+// The KKT inverse is the register-row DPP Gauss-Jordan below.  The
+// matrix-core block Gauss-Jordan forms measured against it (as accurate once
+// made stable, but slower) live in
+// tools/micro/srbd_mfma_inverse.inc with their probe.
 
 namespace qloco {
 
@@ -70,6 +65,9 @@ struct SrbdArgs {
   int max_iter, check_termination, scaling, adaptive_rho, rho_interval;
   float rho_tol;
   int warm_start;
+  // 1: the reference's full 12N-variable QP (every (step, leg) pair is a
+  // variable; swing legs held by fz in [0, 0] rows), 0: stance-only reduction
+  int literal;
   // instances with nlegs outside [leg_lo, leg_hi] belong to the other
   // launch of a split batch (qloco_srbd_solve_ex) and are skipped
   int leg_lo, leg_hi;
@@ -102,23 +100,8 @@ struct SrbdLds {
   f4v bv[NC][2];           // per var: {b0,b1,b2,e0}, {e1,e2,step,comp}
   float xs[NC];            // unscaled x per var (P x)
   float Dc[NC];            // Ruiz column scaling D
-#if QLOCO_SRBD_MFMA_INV
-  union {
-    struct {
-      float err[12 * kMaxN];   // per-step row values (gradient error / aggregates)
-      float Wc[12 * kMaxN];    // per-step Bqp' weights: rows 0..5 W1, rows 6..11 W0
-      f2v k0k2[kMaxN * (kMaxN + 1)];  // [row step][col step]: horizon sums K0, K2
-    };
-    // MFMA inverse staging (clobbers err / Wc / k0k2; the kernel refills
-    // k0k2 after every inverse).  W = 1: the transpose buffer (16 x 68);
-    // W = 2: per-wave transposes (2 x 16 x 68) or the double-buffered
-    // pivot row-block exchange (2 x 8 blocks x 64 lanes x 4)
-    __attribute__((aligned(16))) float sc[W == 1 ? 16 * 68 : 2 * 8 * 256];
-  };
-#else
   float err[12 * kMaxN];   // per-step row values (gradient error / aggregates)
   float Wc[12 * kMaxN];    // per-step Bqp' weights: rows 0..5 W1, rows 6..11 W0
-#endif
   float q2[16];
   float r2[12];
   float x0[16];
@@ -128,9 +111,7 @@ struct SrbdLds {
   float qs[NC];             // per var: scaled q
   int pair[NC];             // per var: 4*step + leg
   int cst[NC];              // per var: step, kMaxN on padding (row of zeros in k0k2)
-#if !QLOCO_SRBD_MFMA_INV
   f2v k0k2[kMaxN * (kMaxN + 1)];  // [row step][col step]: horizon sums K0, K2
-#endif
   float piv[2];
   float colv[W == 1 ? 1 : 2][W == 1 ? 1 : NC];  // W = 2 inverse: pivot column
   float red[W][16];
@@ -554,325 +535,6 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1>
   bsync<1>();
 }
 
-#if QLOCO_SRBD_MFMA_INV
-// ---- KKT inverse on the matrix cores: block Gauss-Jordan.
-// K (64x64 for W = 1, SPD, padding rows/columns diagonal) is held as blocks
-// of 16x16 in the C/D layout of v_mfma_f32_16x16x4_f32: lane (j, g) =
-// 16g + j, register r of block (I, J) = M[16I + 4g + r][16J + j].
-// mfma_tn(Z, Y, C) = Z^T Y + C: the A operand of 16x16x4 (lane l:
-// A[l&15][l>>4]) read from a C-layout block Z gives Z^T when K-slice s takes
-// k = 4g + s, and the B operand (B[l>>4][l&15]) is register s of Y itself;
-// with Y = I it is an exact transpose.  Per block pivot k:
-//  1. the row block k is transposed (Z_J = M_kJ^T) and Gauss-Jordan runs on
-//     its 16 rows with the 16 pivots of the diagonal block (in-place form,
-//     entry-p trick of invert_w1): Z_J -> T_J^T, T_J = M_kk^-1 M_kJ, and
-//     Z_k -> (M_kk^-1)^T.  Elimination, not an explicit inverse times M_kJ:
-//     multiplying by the 16x16 inverse loses a factor cond(M_kk) (measured,
-//     tools/micro/w2_inverse.hip: 2e-1 vs 2.4e-4 at cond 1e4);
-//  2. every other block row I: M_IJ -= M_Ik T_J and M_Ik = -M_Ik M_kk^-1
-//     (MFMA, A operand the exact transpose of the old M_Ik);
-//  3. M_kJ = T_J, M_kk = M_kk^-1.
-// Taking the transposed operands from the symmetry GJ keeps (M_Ik = -+M_kI^T)
-// instead of exact transposes is NOT stable: a float32 emulation gives
-// |K X - I| = 0.67 vs 5e-4 (this form) vs 1e-3 (element GJ) at cond 1e5.
-__device__ __forceinline__ f4v mfma_tn(const f4v &Z, const f4v &Y, f4v C) {
-  C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.x, Y.x, C, 0, 0, 0);
-  C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.y, Y.y, C, 0, 0, 0);
-  C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.z, Y.z, C, 0, 0, 0);
-  C = __builtin_amdgcn_mfma_f32_16x16x4f32(Z.w, Y.w, C, 0, 0, 0);
-  return C;
-}
-__device__ __forceinline__ f4v cident(int lane) {  // 16x16 identity, C layout
-  const int j = lane & 15, g4 = 4 * (lane >> 4);
-  return (f4v){g4 == j ? 1.0f : 0.0f, g4 + 1 == j ? 1.0f : 0.0f, g4 + 2 == j ? 1.0f : 0.0f,
-               g4 + 3 == j ? 1.0f : 0.0f};
-}
-__device__ __forceinline__ f4v ctrans(const f4v &Z, const f4v &Id) {
-  return mfma_tn(Z, Id, (f4v)(0.0f));
-}
-__device__ __forceinline__ float f4get(const f4v &v, int r) {
-  return r == 0 ? v.x : (r == 1 ? v.y : (r == 2 ? v.z : v.w));
-}
-__device__ __forceinline__ void f4set(f4v &v, int r, float x) {
-  if (r == 0) v.x = x; else if (r == 1) v.y = x; else if (r == 2) v.z = x; else v.w = x;
-}
-// Pivot P of the transposed row block Z[0..NB) (lane (a, g) register r of
-// Z_J = M[16k + a][16J + 4g + r]): the pivot by v_readlane, this lane's
-// row coefficient M[16k + a][16k + P] by ds_bpermute (it sits in group P/4),
-// the pivot row entry of this lane's column by DPP row_newbcast:P.
-template <int P, int NB, int k>
-__device__ __forceinline__ void rowblock_pivot(f4v (&Z)[NB], int lane) {
-  constexpr int gq = P >> 2, rq = P & 3;
-  const int a = lane & 15;
-  const float pv = f4get(Z[k], rq);
-  const float piv = __builtin_bit_cast(
-      float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pv), 16 * gq + P));
-  const float pinv = __builtin_amdgcn_rcpf(piv);
-  const float ca = __builtin_bit_cast(
-      float, __builtin_amdgcn_ds_bpermute(4 * (16 * gq + a), __builtin_bit_cast(int, pv)));
-  const float ng = (a == P) ? (pinv - 1.0f) : -(ca * pinv);
-  const bool plane = lane == 16 * gq + P;
-#pragma unroll
-  for (int J = 0; J < NB; ++J) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float src = f4get(Z[J], r);
-      if (J == k && r == rq) src = plane ? piv + 1.0f : src;
-      const float e = dpp<0x150 + P>(src);
-      f4set(Z[J], r, fmaf(ng, e, f4get(Z[J], r)));
-    }
-  }
-}
-template <int NB, int k>
-__device__ __forceinline__ void rowblock_gj(f4v (&Z)[NB], int lane) {
-  rowblock_pivot<0, NB, k>(Z, lane); rowblock_pivot<1, NB, k>(Z, lane);
-  rowblock_pivot<2, NB, k>(Z, lane); rowblock_pivot<3, NB, k>(Z, lane);
-  rowblock_pivot<4, NB, k>(Z, lane); rowblock_pivot<5, NB, k>(Z, lane);
-  rowblock_pivot<6, NB, k>(Z, lane); rowblock_pivot<7, NB, k>(Z, lane);
-  rowblock_pivot<8, NB, k>(Z, lane); rowblock_pivot<9, NB, k>(Z, lane);
-  rowblock_pivot<10, NB, k>(Z, lane); rowblock_pivot<11, NB, k>(Z, lane);
-  rowblock_pivot<12, NB, k>(Z, lane); rowblock_pivot<13, NB, k>(Z, lane);
-  rowblock_pivot<14, NB, k>(Z, lane); rowblock_pivot<15, NB, k>(Z, lane);
-}
-// In-place 16-pivot GJ of one C-layout block (entry-p trick): the pivot row
-// from lane (j, P/4) register P%4 by ds_bpermute, the pivot column from
-// lane P of each 16-lane row by DPP row_newbcast, the pivot by v_readlane.
-template <int P>
-__device__ __forceinline__ void cblock_pivot(f4v &B, int lane) {
-  constexpr int gq = P >> 2, rq = P & 3;
-  const float prow = f4get(B, rq);
-  const float piv = __builtin_bit_cast(
-      float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, prow), 16 * gq + P));
-  const float pinv = __builtin_amdgcn_rcpf(piv);
-  float e = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(
-                                          4 * (16 * gq + (lane & 15)), __builtin_bit_cast(int, prow)));
-  e = ((lane & 15) == P) ? piv + 1.0f : e;
-  const bool pgrp = (lane >> 4) == gq;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float c = dpp<0x150 + P>(f4get(B, r));  // M[4g + r][P]
-    float g = c * pinv;
-    if (r == rq) g = pgrp ? (1.0f - pinv) : g;
-    f4set(B, r, fmaf(-g, e, f4get(B, r)));
-  }
-}
-__device__ __forceinline__ void cblock_inverse(f4v &B, int lane) {
-  cblock_pivot<0>(B, lane); cblock_pivot<1>(B, lane); cblock_pivot<2>(B, lane);
-  cblock_pivot<3>(B, lane); cblock_pivot<4>(B, lane); cblock_pivot<5>(B, lane);
-  cblock_pivot<6>(B, lane); cblock_pivot<7>(B, lane); cblock_pivot<8>(B, lane);
-  cblock_pivot<9>(B, lane); cblock_pivot<10>(B, lane); cblock_pivot<11>(B, lane);
-  cblock_pivot<12>(B, lane); cblock_pivot<13>(B, lane); cblock_pivot<14>(B, lane);
-  cblock_pivot<15>(B, lane);
-}
-#if QLOCO_SRBD_MFMA_INV == 2
-// Explicit-diagonal form: P = M_kk^-1 by the in-block GJ, T_J = P M_kJ on
-// the matrix cores (A operand the exact transpose of P), then the same
-// Schur / column updates with exact transposes of the old M_Ik.
-template <int k>
-__device__ __forceinline__ void gj_block_step(f4v (&M)[4][4], int lane, const f4v &Id) {
-  cblock_inverse(M[k][k], lane);
-  const f4v P = M[k][k];
-  const f4v Pt = ctrans(P, Id);
-  f4v nT[4];
-#pragma unroll
-  for (int J = 0; J < 4; ++J)
-    if (J != k) nT[J] = -mfma_tn(Pt, M[k][J], (f4v)(0.0f));
-  const f4v nP = -P;
-#pragma unroll
-  for (int I = 0; I < 4; ++I) {
-    if (I == k) continue;
-    const f4v ZI = ctrans(M[I][k], Id);  // old M_Ik^T
-#pragma unroll
-    for (int J = 0; J < 4; ++J)
-      if (J != k) M[I][J] = mfma_tn(ZI, nT[J], M[I][J]);
-    M[I][k] = mfma_tn(ZI, nP, (f4v)(0.0f));
-  }
-#pragma unroll
-  for (int J = 0; J < 4; ++J)
-    if (J != k) M[k][J] = -nT[J];
-}
-#else
-template <int k>
-__device__ __forceinline__ void gj_block_step(f4v (&M)[4][4], int lane, const f4v &Id) {
-  f4v Z[4];
-#pragma unroll
-  for (int J = 0; J < 4; ++J) Z[J] = ctrans(M[k][J], Id);
-  rowblock_gj<4, k>(Z, lane);
-  f4v nT[4];
-#pragma unroll
-  for (int J = 0; J < 4; ++J) nT[J] = -ctrans(Z[J], Id);  // nT[k] = -M_kk^-1
-#pragma unroll
-  for (int I = 0; I < 4; ++I) {
-    if (I == k) continue;
-    const f4v ZI = ctrans(M[I][k], Id);  // old M_Ik^T
-#pragma unroll
-    for (int J = 0; J < 4; ++J)
-      if (J != k) M[I][J] = mfma_tn(ZI, nT[J], M[I][J]);
-    M[I][k] = mfma_tn(ZI, nT[k], (f4v)(0.0f));
-  }
-#pragma unroll
-  for (int J = 0; J < 4; ++J) M[k][J] = -nT[J];
-}
-#endif
-// Row layout in and out (lane v holds row v of K, then of K^-1) through a
-// transpose buffer tb[c][row] of 16 columns at a time.  The computed K^-1 is
-// not exactly symmetric, so no entry is taken from its mirror (reading
-// M[r][c] from row c was measured ~1000x less accurate at cond 1e5).
-// Block pivots past the valid columns (ncol) are identity-padding blocks
-// and are skipped (their rows / columns carry zeros off the diagonal).
-__device__ __forceinline__ void invert_w1_mfma(SrbdLds<1> &S, int t, int ncol, Row<1> &K) {
-  const int lane = t & 63, j = lane & 15, g = lane >> 4;
-  const int nb = (__builtin_amdgcn_readfirstlane(ncol) + 15) >> 4;
-  float *tb = S.sc;
-  f4v M[4][4];
-  bsync<1>();
-#pragma unroll
-  for (int J = 0; J < 4; ++J) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) tb[c * 68 + lane] = K.k[16 * J + c];
-    bsync<1>();
-#pragma unroll
-    for (int I = 0; I < 4; ++I) M[I][J] = *reinterpret_cast<const f4v *>(&tb[j * 68 + 16 * I + 4 * g]);
-    bsync<1>();
-  }
-  const f4v Id = cident(lane);
-  gj_block_step<0>(M, lane, Id);
-  if (nb > 1) gj_block_step<1>(M, lane, Id);
-  if (nb > 2) gj_block_step<2>(M, lane, Id);
-  if (nb > 3) gj_block_step<3>(M, lane, Id);
-#pragma unroll
-  for (int J = 0; J < 4; ++J) {
-#pragma unroll
-    for (int I = 0; I < 4; ++I) *reinterpret_cast<f4v *>(&tb[j * 68 + 16 * I + 4 * g]) = M[I][J];
-    bsync<1>();
-#pragma unroll
-    for (int c = 0; c < 16; ++c) K.k[16 * J + c] = tb[c * 68 + lane];
-    bsync<1>();
-  }
-}
-
-// ---- W = 2 inverse on the matrix cores: the same block Gauss-Jordan over
-// 8 x 8 blocks; wave w holds block rows 4w..4w+3 (its 64 K rows) in the C
-// layout.  Per block pivot k the owning wave eliminates its transposed row
-// block and publishes Z_J = T_J^T through LDS, one barrier, then both waves
-// update their own block rows (each transposes the Z_J it needs); the
-// buffer alternates with k, so a wave may run ahead into step k + 1 safely.
-#if QLOCO_SRBD_MFMA_INV == 2
-template <int k, int w>
-__device__ __forceinline__ void gj2_step(SrbdLds<2> &S, f4v (&M)[4][8], int lane, const f4v &Id) {
-  constexpr int ow = k >> 2, ik = k & 3;
-  f4v *xb = reinterpret_cast<f4v *>(S.sc) + (k & 1) * 8 * 64;  // [block J][lane]: old row block k, P at J = k
-  if constexpr (w == ow) {
-    cblock_inverse(M[ik][k], lane);
-#pragma unroll
-    for (int J = 0; J < 8; ++J) xb[J * 64 + lane] = M[ik][J];
-  }
-  f4v ZI[4];  // old M_Ik^T of this wave's block rows
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (4 * w + i != k) ZI[i] = ctrans(M[i][k], Id);
-  __syncthreads();
-  const f4v P = (w == ow) ? M[ik][k] : xb[k * 64 + lane];
-  const f4v Pt = ctrans(P, Id);
-#pragma unroll
-  for (int J = 0; J < 8; ++J) {
-    if (J == k) continue;
-    const f4v OJ = (w == ow) ? M[ik][J] : xb[J * 64 + lane];
-    const f4v nT = -mfma_tn(Pt, OJ, (f4v)(0.0f));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (4 * w + i != k) M[i][J] = mfma_tn(ZI[i], nT, M[i][J]);
-    if constexpr (w == ow) M[ik][J] = -nT;
-  }
-  const f4v nP = -P;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (4 * w + i != k) M[i][k] = mfma_tn(ZI[i], nP, (f4v)(0.0f));
-}
-#else
-template <int k, int w>
-__device__ __forceinline__ void gj2_step(SrbdLds<2> &S, f4v (&M)[4][8], int lane, const f4v &Id) {
-  constexpr int ow = k >> 2, ik = k & 3;
-  f4v *xb = reinterpret_cast<f4v *>(S.sc) + (k & 1) * 8 * 64;  // [block J][lane]
-  f4v Z[8];
-  if constexpr (w == ow) {
-#pragma unroll
-    for (int J = 0; J < 8; ++J) Z[J] = ctrans(M[ik][J], Id);
-    rowblock_gj<8, k>(Z, lane);
-#pragma unroll
-    for (int J = 0; J < 8; ++J) xb[J * 64 + lane] = Z[J];
-  }
-  f4v ZI[4];  // old M_Ik^T of this wave's block rows
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (4 * w + i != k) ZI[i] = ctrans(M[i][k], Id);
-  __syncthreads();
-#pragma unroll
-  for (int J = 0; J < 8; ++J) {
-    if (J == k) continue;
-    const f4v ZJ = (w == ow) ? Z[J] : xb[J * 64 + lane];
-    const f4v nT = -ctrans(ZJ, Id);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (4 * w + i != k) M[i][J] = mfma_tn(ZI[i], nT, M[i][J]);
-    if constexpr (w == ow) M[ik][J] = -nT;
-  }
-  const f4v nP = -ctrans((w == ow) ? Z[k] : xb[k * 64 + lane], Id);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (4 * w + i != k) M[i][k] = mfma_tn(ZI[i], nP, (f4v)(0.0f));
-  if constexpr (w == ow) M[ik][k] = -nP;
-}
-#endif
-template <int w>
-__device__ __forceinline__ void gj2_steps(SrbdLds<2> &S, f4v (&M)[4][8], int lane, int nb) {
-  const f4v Id = cident(lane);
-  gj2_step<0, w>(S, M, lane, Id);
-  gj2_step<1, w>(S, M, lane, Id);
-  gj2_step<2, w>(S, M, lane, Id);
-  gj2_step<3, w>(S, M, lane, Id);
-  if (nb > 4) gj2_step<4, w>(S, M, lane, Id);
-  if (nb > 5) gj2_step<5, w>(S, M, lane, Id);
-  if (nb > 6) gj2_step<6, w>(S, M, lane, Id);
-  if (nb > 7) gj2_step<7, w>(S, M, lane, Id);
-}
-// Row layout in and out through a per-wave transpose buffer (tb[c][row]:
-// 16 columns of the wave's 64 rows); block pivots past the valid columns of
-// the second half are identity-padding blocks and are skipped.
-__device__ __forceinline__ void invert_w2_mfma(SrbdLds<2> &S, int t, int ncol1, Row<2> &K) {
-  const int wave = t >> 6, lane = t & 63, j = lane & 15, g = lane >> 4;
-  const int nb = 4 + ((__builtin_amdgcn_readfirstlane(ncol1) + 15) >> 4);
-  float *tb = S.sc + wave * (16 * 68);
-  f4v M[4][8];
-  __syncthreads();
-#pragma unroll
-  for (int J = 0; J < 8; ++J) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) tb[c * 68 + lane] = K.k[16 * J + c];
-    bsync<1>();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) M[i][J] = *reinterpret_cast<const f4v *>(&tb[j * 68 + 16 * i + 4 * g]);
-    bsync<1>();
-  }
-  __syncthreads();
-  if (wave == 0)
-    gj2_steps<0>(S, M, lane, nb);
-  else
-    gj2_steps<1>(S, M, lane, nb);
-  __syncthreads();
-#pragma unroll
-  for (int J = 0; J < 8; ++J) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<f4v *>(&tb[j * 68 + 16 * i + 4 * g]) = M[i][J];
-    bsync<1>();
-#pragma unroll
-    for (int c = 0; c < 16; ++c) K.k[16 * J + c] = tb[c * 68 + lane];
-    bsync<1>();
-  }
-  __syncthreads();
-}
-
-#endif  // QLOCO_SRBD_MFMA_INV
 
 // K0 / K2 table over (row step, column step); column kMaxN is the zero row
 // of padding lanes (cst = kMaxN)
@@ -915,12 +577,8 @@ __device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, int
     const float g = (tt == k) ? (1.0f - pinv) : v * pinv;
     const float ng = -g;
     QL_DPP_GJ64(K.k, 0, r0, ng);
-#if QLOCO_W2_GJ_BUCKETS
-    QL_HALF2(c2, QL_DPP_GJ36, QL_DPP_GJ60, QL_DPP_GJ64, K.k, 64, r1, ng);  // uniform branch
-#else
-    (void)c2;  // one form: three per pivot triple the (instruction-cache bound) code
+    (void)c2;  // one form: per-bucket forms triple the (instruction-cache bound) code
     QL_DPP_GJ64(K.k, 64, r1, ng);
-#endif
   }
 }
 
@@ -1009,10 +667,11 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
   }
   bsync<W>();
 
-  // ---------------- 2. stance enumeration (integer, bit-exact)
+  // ---------------- 2. variable enumeration (integer, bit-exact): the stance
+  // (step, leg) pairs, or every pair for the literal full QP
   if (wave == 0) {
-    const bool s0 = (lane < 4 * N) && S.ct[lane];
-    const bool s1 = (64 + lane < 4 * N) && S.ct[64 + lane];
+    const bool s0 = (lane < 4 * N) && (a.literal || S.ct[lane]);
+    const bool s1 = (64 + lane < 4 * N) && (a.literal || S.ct[64 + lane]);
     const uint64_t m0 = __ballot(s0), m1 = __ballot(s1);
     const uint64_t below = (1ull << lane) - 1ull;
     const int c0 = __popcll(m0);
@@ -1050,8 +709,13 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
   bool p_init = false, p_same = false;
   if (prec) {
     p_init = prec[NP + 1] > 0.5f;
+    // literal full QP: the problem structure never changes (the reference's
+    // Hessian pattern is contact-independent, ConvexMpc.cpp:211-215), so
+    // every call after the first takes the update path; the stance-only
+    // reduction re-initialises when its variable set changes
     int mism = 0;
-    for (int k = t; k < 4 * N; k += 64 * W) mism |= (prec[96 * N + k] != 0.0f) != (S.ct[k] != 0);
+    if (!a.literal)
+      for (int k = t; k < 4 * N; k += 64 * W) mism |= (prec[96 * N + k] != 0.0f) != (S.ct[k] != 0);
     p_same = p_init && !__syncthreads_or(mism);
   }
   int ncol[W];
@@ -1174,8 +838,11 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
   const bool xy = comp < 2;
   float ra0 = valid ? 1.0f : 0.0f, ra1 = (valid && xy) ? 1.0f : 0.0f;
   float rz0 = (valid && xy) ? a.mu : 0.0f, rz1 = (valid && xy) ? -a.mu : 0.0f;
-  const float rl0 = !valid ? 0.0f : (xy ? 0.0f : a.fz_min);
-  const float ru0 = !valid ? 0.0f : (xy ? INFINITY : a.fz_max);
+  // fz in [fz_min * c, fz_max * c] (:237, :242): c = 1 on every stance pair,
+  // 0 on the swing pairs the literal full QP keeps
+  const float cflag = valid ? (float)S.ct[4 * step + leg] : 0.0f;
+  const float rl0 = !valid ? 0.0f : (xy ? 0.0f : a.fz_min * cflag);
+  const float ru0 = !valid ? 0.0f : (xy ? INFINITY : a.fz_max * cflag);
   float rE0 = 1.0f, rE1 = 1.0f, Dr = 1.0f, cs = 1.0f;
   S.aux[0][t] = r2v;
   S.pair[t] = 4 * step + leg;
@@ -1380,11 +1047,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
       if (first) QL_PHASE(5);
       if constexpr (W == 1) {
         (void)dg;
-#if QLOCO_SRBD_MFMA_INV && (QLOCO_SRBD_MFMA_W & 1)  // matrix-core block Gauss-Jordan
-        invert_w1_mfma(S, t, ncol[0], K);
-        fill_k0k2<1>(S, N, Nf, t);  // the staging buffer overlaid the K0 / K2 table
-        bsync<1>();
-#else
         if (c60) {
           invert_w1<true>(S, t, ncol[0], K);
 #ifdef QLOCO_ABLATE_DUP_INV  // timing experiments only: K^-1 -> K -> K^-1
@@ -1394,16 +1056,9 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
         } else {
           invert_w1<false>(S, t, ncol[0], K);
         }
-#endif
       } else {
         (void)dg;
-#if QLOCO_SRBD_MFMA_INV && (QLOCO_SRBD_MFMA_W & 2)
-        invert_w2_mfma(S, t, ncol[1], K);
-        fill_k0k2<2>(S, N, Nf, t);
-        __syncthreads();
-#else
         invert_w2(S, t, ncol, c2, K);
-#endif
       }
       if (first) QL_PHASE(6);
     }
@@ -1700,7 +1355,9 @@ __global__ __launch_bounds__(256) void srbd_classify_kernel(const SrbdArgs a, in
   int cls = -1;
   if (b < a.batch) {
     int legs = 0;
-    if (a.contacts_per_step) {
+    if (a.literal) {
+      legs = 4 * N;
+    } else if (a.contacts_per_step) {
       const uint8_t *c = a.contacts + b * 4 * N;
       for (int k = 0; k < 4 * N; ++k) legs += c[k] != 0;
     } else {
@@ -1771,10 +1428,16 @@ extern "C" int qloco_phase_read(unsigned int *host, size_t count) {
 }
 #endif
 
-// Per-device scratch of the class dispatch: three instance lists of `cap`
-// entries, their counters, two side streams and the fork / join events.
-// Grown (never shrunk) under a mutex; a grow waits for the device first, as
-// in-flight launches may still read the old lists.
+// Scratch of the class dispatch: three instance lists of `cap` entries, their
+// counters, two side streams and the fork / join events -- one set per
+// (device, caller stream), so calls on different streams or threads never
+// share lists, counters or events (two calls on ONE stream are ordered by
+// it).  A captured HIP graph bakes the list pointers in, so a buffer is never
+// freed while the process lives: a larger batch allocates a new set and
+// retires the old one (kept, not freed -- no device-wide synchronisation on
+// the grow path either).  Growing inside a stream capture is refused
+// (QLOCO_ERR_ARG): run the largest batch once before capturing
+// (INTEGRATION.md).
 struct SrbdScratch {
   int *lists = nullptr;
   int *counts = nullptr;
@@ -1783,35 +1446,44 @@ struct SrbdScratch {
   hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
 };
 static std::mutex g_srbd_scratch_mu;
-static SrbdScratch g_srbd_scratch[64];
+static std::map<std::pair<int, hipStream_t>, SrbdScratch> g_srbd_scratch;
+static std::vector<void *> g_srbd_retired;  // outgrown lists (a graph may still read them)
 
-static SrbdScratch *srbd_scratch(int64_t batch) {
+// Caller holds g_srbd_scratch_mu for the whole enqueue sequence (counter
+// reset, classification, class launches): two threads sharing one stream
+// must not interleave their sequences on the shared counters.
+static int srbd_scratch(int64_t batch, hipStream_t st, SrbdScratch **out) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> lk(g_srbd_scratch_mu);
-  SrbdScratch &s = g_srbd_scratch[dev];
-  if (!s.counts) {
-    if (hipMalloc(&s.counts, 4 * sizeof(int)) != hipSuccess) return nullptr;
-    for (int k = 0; k < 2; ++k) {
-      if (hipStreamCreateWithFlags(&s.side[k], hipStreamNonBlocking) != hipSuccess) return nullptr;
-      if (hipEventCreateWithFlags(&s.join[k], hipEventDisableTiming) != hipSuccess) return nullptr;
+  if (hipGetDevice(&dev) != hipSuccess) return QLOCO_ERR_DEVICE;
+  SrbdScratch &s = g_srbd_scratch[std::make_pair(dev, st)];
+  const bool fresh = !s.counts;
+  if (fresh || batch > s.cap) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+      set_last_error("qloco_srbd_solve_ex: class-dispatch scratch must be sized before stream "
+                     "capture (run the largest batch once on this stream first)",
+                     hipErrorStreamCaptureUnsupported);
+      return QLOCO_ERR_ARG;
     }
-    if (hipEventCreateWithFlags(&s.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+  }
+  if (fresh) {
+    if (hipMalloc(&s.counts, 4 * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
+    for (int k = 0; k < 2; ++k) {
+      if (hipStreamCreateWithFlags(&s.side[k], hipStreamNonBlocking) != hipSuccess) return QLOCO_ERR_DEVICE;
+      if (hipEventCreateWithFlags(&s.join[k], hipEventDisableTiming) != hipSuccess) return QLOCO_ERR_DEVICE;
+    }
+    if (hipEventCreateWithFlags(&s.fork, hipEventDisableTiming) != hipSuccess) return QLOCO_ERR_DEVICE;
   }
   if (batch > s.cap) {
-    if (s.lists) {
-      if (hipDeviceSynchronize() != hipSuccess) return nullptr;
-      (void)hipFree(s.lists);
-      s.lists = nullptr;
-    }
     const int64_t cap = batch < 4096 ? 4096 : batch;
-    if (hipMalloc(&s.lists, 3 * cap * sizeof(int)) != hipSuccess) {
-      s.cap = 0;
-      return nullptr;
-    }
+    int *lists = nullptr;
+    if (hipMalloc(&lists, 3 * cap * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
+    if (s.lists) g_srbd_retired.push_back(s.lists);
+    s.lists = lists;
     s.cap = cap;
   }
-  return &s;
+  *out = &s;
+  return QLOCO_OK;
 }
 
 // Concurrent class launches (default) or all on the caller's stream
@@ -1840,6 +1512,7 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   // enables it, A1RobotControl.cpp:558-559) is not implemented: refuse rather
   // than return unpolished iterates as if polished
   if (spec->polish) return QLOCO_ERR_ARG;
+  if (spec->literal_full_qp < 0 || spec->literal_full_qp > 1) return QLOCO_ERR_ARG;
   SrbdArgs a;
   memset(&a, 0, sizeof(a));
   a.N = spec->horizon;
@@ -1866,6 +1539,7 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   a.rho_interval = spec->adaptive_rho_interval;
   a.rho_tol = spec->adaptive_rho_tolerance;
   a.warm_start = spec->warm_start;
+  a.literal = spec->literal_full_qp ? 1 : 0;
   a.batch = batch;
   a.x0 = x0;
   a.xref = x_ref;
@@ -1889,7 +1563,8 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   // one class's tail overlaps another's bulk.  The top class the caller's
   // maximum admits takes every instance above the lower classes, so an
   // instance beyond a too-small maximum gets QLOCO_BAD_SIZE there.
-  const int legs = max_stance_legs > 0 ? max_stance_legs : 4 * spec->horizon;
+  // the literal full QP has 4N "legs" (variable triples) in every instance
+  const int legs = (a.literal || max_stance_legs <= 0) ? 4 * spec->horizon : max_stance_legs;
   hipStream_t st = (hipStream_t)stream;
   a.leg_lo = 0;
   a.leg_hi = 1 << 30;
@@ -1924,8 +1599,10 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   if (top == 0) {
     launch(0, st);
   } else {
-    SrbdScratch *sc = srbd_scratch(batch);
-    if (!sc) return QLOCO_ERR_DEVICE;
+    std::lock_guard<std::mutex> lk(g_srbd_scratch_mu);
+    SrbdScratch *sc = nullptr;
+    const int rc = srbd_scratch(batch, st, &sc);
+    if (rc != QLOCO_OK) return rc;
     QLOCO_HIP_CHECK(hipMemsetAsync(sc->counts, 0, 4 * sizeof(int), st), "class counters");
     hipLaunchKernelGGL(srbd_classify_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st,
                        a, top, sc->lists, sc->cap, sc->counts);

@@ -75,8 +75,11 @@ QPsolverGpu::QPsolverGpu(int max_batch) : max_batch_(max_batch < 1 ? 1 : max_bat
 QPsolverGpu::~QPsolverGpu() = default;
 
 void QPsolverGpu::resize(const int &nVar, const int &nEq, const int &nIneq) {
-  // QPBaseClass.cpp:111-112 asserts the sizes; here they are the kernel's limits
-  if (nVar < 1 || nVar > qloco_max_gi_vars() || nEq < 0 || nEq > 16 || nIneq < 0 || nIneq > 64)
+  // QPBaseClass.cpp:111-112 asserts nVars <= 60, nIneq <= 300; the kernels
+  // take n, p <= 64, m <= 320 (qloco_gi_limits)
+  int32_t ln = 0, lp = 0, lm = 0;
+  qloco_gi_limits(&ln, &lp, &lm);
+  if (nVar < 1 || nVar > ln || nEq < 0 || nEq > lp || nIneq < 0 || nIneq > lm)
     throw Error("QPsolverGpu::resize: size out of range", QLOCO_BAD_SIZE);
   n_ = nVar;
   p_ = nEq;
@@ -378,7 +381,16 @@ ConvexMpcBatch::ConvexMpcBatch(int batch, const qloco_srbd_spec *sp)
   } else {
     qloco_srbd_spec_default(&spec);
     spec.warm_start = 2;       // the reference's persistent member solver
+    spec.literal_full_qp = 1;  // on its literal 12N-variable QP (update path every call)
   }
+  if (spec.horizon < 1 || spec.horizon > 20)
+    throw Error("ConvexMpcBatch: horizon outside 1..20", QLOCO_BAD_SIZE);
+  if (spec.warm_start < 0 || spec.warm_start > 2)
+    throw Error("ConvexMpcBatch: warm_start outside 0..2", QLOCO_ERR_ARG);
+  // the device buffers (x_ref, the persistent record) are sized from these:
+  // later edits of the public spec are checked against them on every call
+  horizon_ = spec.horizon;
+  warm_mode_ = spec.warm_start;
   spec.feet_per_step = 0;      // compute_grf passes one foot_pos_abs (:527-531)
   spec.contacts_per_step = 0;  // and one contacts[4] (ConvexMpc.cpp:232-249)
   spec.output_frame = 1;       // root_rot_mat' u (:596-599)
@@ -398,25 +410,34 @@ ConvexMpcBatch::ConvexMpcBatch(int batch, const qloco_srbd_spec *sp)
   iters.assign(B, 0);
 }
 
+void ConvexMpcBatch::check_spec() const {
+  if (spec.horizon != horizon_)
+    throw Error("ConvexMpcBatch: spec.horizon changed after construction (buffers sized for " +
+                    std::to_string(horizon_) + ")", QLOCO_ERR_ARG);
+  if (spec.warm_start != warm_mode_)
+    throw Error("ConvexMpcBatch: spec.warm_start changed after construction", QLOCO_ERR_ARG);
+}
+
 void ConvexMpcBatch::reset() {
   if (!d_rec_) return;
   hip_ok(hipMemsetAsync(d_rec_, 0,
-                        sizeof(float) * (size_t)batch_ * QLOCO_SRBD_PERSIST_LEN(spec.horizon),
+                        sizeof(float) * (size_t)batch_ * QLOCO_SRBD_PERSIST_LEN(horizon_),
                         (hipStream_t)arena_.stream()),
          "hipMemsetAsync");
 }
 
 void ConvexMpcBatch::solve_device(const float *x0, const float *x_ref, const float *feet,
                                   const uint8_t *contacts, float *u0, int32_t *st, int32_t *it) {
-  int32_t legs = 0;  // constant contacts over the horizon: max stance legs = 4N worst case
-  legs = 4 * spec.horizon;
+  check_spec();
+  const int32_t legs = 4 * horizon_;  // constant contacts over the horizon: 4N worst case
   abi_ok(qloco_srbd_solve_ex(&spec, batch_, x0, x_ref, feet, contacts, u0, nullptr, st, it,
                              nullptr, nullptr, d_rec_, legs, arena_.stream()),
          "qloco_srbd_solve_ex");
 }
 
 void ConvexMpcBatch::compute_grf(const A1MpcState *s, double *forces) {
-  const size_t B = batch_, N = spec.horizon;
+  check_spec();
+  const size_t B = batch_, N = horizon_;
   const double dt = spec.dt;
   std::vector<float> x0(B * 13), xr(B * 13 * N), feet(B * 12);
   std::vector<uint8_t> ct(B * 4);

@@ -27,20 +27,24 @@ def _stream(t):
     return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
-def _check_rows(name, t, shape, device=None):
+def _check_rows(rows, device):
     """The tick kernels read shape[1] doubles per robot row straight from the
     device pointer: anything but a contiguous float64 tensor of exactly that
     shape on the node's device would be read out of bounds (or a host address
-    dereferenced on the GPU), so it is rejected here, before any launch."""
+    dereferenced on the GPU), so it is rejected here, before any launch.
+    rows: (name, tensor, shape) triples; every layout is checked before any
+    device, so a malformed message is named even when both sit on the host."""
     import torch
-    if not isinstance(t, torch.Tensor):
-        raise ValueError("%s: expected a torch tensor, got %s" % (name, type(t).__name__))
-    if tuple(t.shape) != tuple(shape) or t.dtype != torch.float64 or not t.is_contiguous():
-        raise ValueError("%s: expected contiguous float64 %s, got %s %s%s" % (
-            name, tuple(shape), t.dtype, tuple(t.shape),
-            "" if t.is_contiguous() else " (non-contiguous)"))
-    if device is not None and t.device != torch.device(device):
-        raise ValueError("%s: on %s, the node batch lives on %s" % (name, t.device, device))
+    for name, t, shape in rows:
+        if not isinstance(t, torch.Tensor):
+            raise ValueError("%s: expected a torch tensor, got %s" % (name, type(t).__name__))
+        if tuple(t.shape) != tuple(shape) or t.dtype != torch.float64 or not t.is_contiguous():
+            raise ValueError("%s: expected contiguous float64 %s, got %s %s%s" % (
+                name, tuple(shape), t.dtype, tuple(t.shape),
+                "" if t.is_contiguous() else " (non-contiguous)"))
+    for name, t, _ in rows:
+        if t.device != torch.device(device):
+            raise ValueError("%s: on %s, the node batch lives on %s" % (name, t.device, device))
 
 
 class RtNodeBatch:
@@ -66,10 +70,8 @@ class RtNodeBatch:
     def tick(self, gait_msg, ctrl_msg, with_debug=True, stream=None):
         """One loop iteration; gait_msg (B,100), ctrl_msg (B,25) float64 device
         tensors.  Returns (traj, nrt, gen, sched) device tensors (reused)."""
-        _check_rows("gait_msg", gait_msg, (self.batch, GAIT_LEN))
-        _check_rows("ctrl_msg", ctrl_msg, (self.batch, CTRL_LEN))
-        _check_rows("gait_msg", gait_msg, (self.batch, GAIT_LEN), self.device)
-        _check_rows("ctrl_msg", ctrl_msg, (self.batch, CTRL_LEN), self.device)
+        _check_rows((("gait_msg", gait_msg, (self.batch, GAIT_LEN)),
+                     ("ctrl_msg", ctrl_msg, (self.batch, CTRL_LEN))), self.device)
         s = _stream(self.ws) if stream is None else stream
         check(lib().qloco_rt_tick(self.batch, ptr(self.ws), ptr(gait_msg), ptr(ctrl_msg),
                                   ptr(self.traj), ptr(self.nrt),

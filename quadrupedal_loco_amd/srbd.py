@@ -84,7 +84,10 @@ class BatchedConvexMpc:
 
     solve() enqueues one kernel on `stream` (default: torch's current
     stream) and returns device tensors; nothing is synchronised unless
-    `max_legs` has to be computed from the contacts.
+    `max_legs` has to be computed from the contacts.  literal_full_qp=1
+    solves the reference's 12N-variable QP as written (swing forces as
+    ADMM variables held at [0, 0]); the default 0 solves the stance-only
+    reduction (same optimum, fewer variables).
     """
 
     def __init__(self, spec=None, **overrides):
@@ -122,7 +125,9 @@ class BatchedConvexMpc:
             raise ValueError("x0 (B,13) and x_ref (B,13N) expected")
         self.spec.feet_per_step = 1 if feet.shape[1] == 12 * N and N > 1 else 0
         self.spec.contacts_per_step = 1 if contacts.shape[1] == 4 * N and N > 1 else 0
-        if max_legs is None:
+        if self.spec.literal_full_qp:  # every (step, leg) pair is a variable
+            max_legs = 4 * N
+        elif max_legs is None:
             max_legs = max_stance_legs(contacts, N, bool(self.spec.contacts_per_step))
         if out is None:
             out = self.alloc_outputs(B, x0.device, full=full)
@@ -170,9 +175,13 @@ class PersistentConvexMpc(BatchedConvexMpc):
     up, later ones take OSQP's update path -- new P / q / bounds into the
     live workspace, Ruiz recomputed with the previous gradient in the cost
     scale, the adapted rho and the scaled iterates carried over
-    (A1RobotControl.cpp:556-578).  A controller whose stance set changes is
-    re-initialised and warm-started from its last solution.  The per-instance
-    record lives on the device (`record`, zeroed by reset())."""
+    (A1RobotControl.cpp:556-578).  With literal_full_qp=1 (the reference's
+    12N-variable problem) that holds for every call after the first, stance
+    changes included (the bounds update re-types the fz rows); on the
+    stance-only reduction (literal_full_qp=0) a controller whose stance set
+    changes is re-initialised and warm-started from its last solution
+    (DESIGN.md §3c).  The per-instance record lives on the device
+    (`record`, zeroed by reset())."""
 
     def __init__(self, batch, device, spec=None, **overrides):
         import torch

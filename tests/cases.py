@@ -25,13 +25,15 @@ def force_inputs(rng, B):
                 FT_total_des=F_sum, mode=mode, right_support=rs, y_coef=y)
 
 
-def closed_loop_srbd(N, B, ticks, seed=20261015, switch_at=None, gait="trot"):
+def closed_loop_srbd(N, B, ticks, seed=20261015, switch_at=None, gait="trot", switch_every=None):
     """A control-loop sequence of SRBD MPC inputs (float32, per tick): the
     synthetic trot instances drift as the robot would between 2.5 ms MPC
     ticks (position by v dt, attitude by omega dt, the reference trajectory
     moving with them), and from tick `switch_at` on the even controllers
-    switch phase (contacts flipped: their stance set changes, the persistent
-    solver's re-initialisation path).  Returns a list of (x0, x_ref, feet, contacts)."""
+    switch phase (contacts flipped: their stance set changes).  With
+    `switch_every` = K every controller flips its trot phase each K ticks
+    (odd controllers offset by K // 2): a gait's phase switches.  Returns a
+    list of (x0, x_ref, feet, contacts)."""
     from quadrupedal_loco_amd import srbd
     x0, xr, ft, ct = srbd.generate(seed, N, B, gait)
     dt = 0.0025
@@ -48,5 +50,12 @@ def closed_loop_srbd(N, B, ticks, seed=20261015, switch_at=None, gait="trot"):
         c = ct.copy()
         if switch_at is not None and t >= switch_at:
             c[0::2] = 1 - c[0::2]
+        if switch_every:
+            flip = (t // switch_every) % 2 == 1
+            flip_odd = ((t + switch_every // 2) // switch_every) % 2 == 1
+            if flip:
+                c[0::2] = 1 - c[0::2]
+            if flip_odd:
+                c[1::2] = 1 - c[1::2]
         seq.append((x.astype(np.float32), r.reshape(B, 13 * N).astype(np.float32), ft.copy(), c))
     return seq

@@ -58,9 +58,9 @@ int main() {
   qloco_a1_params_default(&ap);
   CHECK(qloco_a1_qp_solve(&ap, -1, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                           nullptr, nullptr) == QLOCO_ERR_ARG, "a1 batch -1");
-  CHECK(qloco_eiquadprog_solve(17, 0, 8, 1, nullptr, 0, nullptr, 0, nullptr, 0, nullptr, 0, nullptr,
+  CHECK(qloco_eiquadprog_solve(65, 0, 8, 1, nullptr, 0, nullptr, 0, nullptr, 0, nullptr, 0, nullptr,
                                0, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
-                               nullptr) == QLOCO_BAD_SIZE, "eiquadprog n 17");
+                               nullptr) == QLOCO_BAD_SIZE, "eiquadprog n 65");
   CHECK(qloco_rt_workspace_bytes(-1) == -1, "rt ws");
   CHECK(qloco_servo_workspace_bytes(-1) == -1, "servo ws");
   CHECK(std::string(qloco_status_string(QLOCO_BAD_SIZE)).size() > 0, "status string");

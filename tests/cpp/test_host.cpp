@@ -104,13 +104,22 @@ static void test_force_qp() {
   std::printf("force QP ok (config 1 total fz %.4f N)\n", fz);
 }
 
+static void test_qpsolver_size(int n, int p, int m, int trials, int zero_ce);
 static void test_qpsolver() {
-  std::mt19937_64 rng(11);
+  test_qpsolver_size(12, 3, 24, 20, 0);
+  // QPBaseClass's capacity (nVars <= 60, nIneq <= 300, QPBaseClass.h:49-51):
+  // the one-QP-per-wavefront kernel, zero CE columns included
+  test_qpsolver_size(60, 10, 300, 4, 3);
+  test_qpsolver_size(30, 0, 120, 4, 0);
+  std::printf("QPsolver ok\n");
+}
+
+static void test_qpsolver_size(int n, int p, int m, int trials, int zero_ce) {
+  std::mt19937_64 rng(11 + n);
   std::normal_distribution<double> N01(0.0, 1.0);
-  const int n = 12, p = 3, m = 24;
   qloco::QPBaseClassGpu qp;
   qp.resizeQP(n, p, m);
-  for (int trial = 0; trial < 20; ++trial) {
+  for (int trial = 0; trial < trials; ++trial) {
     std::vector<double> M(n * n);
     for (auto &v : M) v = N01(rng);
     for (int r = 0; r < n; ++r)
@@ -121,6 +130,10 @@ static void test_qpsolver() {
       }
     for (auto &v : qp.g0) v = 3.0 * N01(rng);
     for (auto &v : qp.CE) v = N01(rng);
+    for (int z = 0; z < zero_ce && p > 0; ++z) {  // EiQuadProg skips all-zero CE columns
+      const int c = (int)(rng() % (uint64_t)p);
+      for (int r = 0; r < n; ++r) qp.CE[c * n + r] = 0.0;
+    }
     for (auto &v : qp.ce0) v = 0.3 * N01(rng);
     for (auto &v : qp.CI) v = N01(rng);
     for (auto &v : qp.ci0) v = N01(rng) + 0.5;
@@ -133,13 +146,12 @@ static void test_qpsolver() {
     const bool ok = qp.solveQP();
     bool ref_ok = true;  // QPBaseClass.cpp:137-150: success = no NaN in X
     for (double v : x) ref_ok = ref_ok && !std::isnan(v);
-    CHECK(ok == ref_ok, "QPBaseClass success flag trial %d", trial);
+    CHECK(ok == ref_ok, "QPBaseClass success flag (%d,%d,%d) trial %d", n, p, m, trial);
     if (st == QO_OK)
       for (int k = 0; k < n; ++k)
-        CHECK(close(qp.X[k], x[k], 1e-9, 1e-9), "QP x trial %d [%d] %.12g vs %.12g", trial, k,
-              qp.X[k], x[k]);
+        CHECK(close(qp.X[k], x[k], 1e-9, 1e-9), "QP (%d,%d,%d) x trial %d [%d] %.12g vs %.12g", n,
+              p, m, trial, k, qp.X[k], x[k]);
   }
-  std::printf("QPsolver ok\n");
 }
 
 static void test_body_mpc() {
@@ -224,6 +236,7 @@ static void test_convex_mpc() {
 static void test_convex_mpc_persistent() {
   qloco::ConvexMpcBatch mpc(2);
   CHECK(mpc.spec.warm_start == 2, "default ConvexMpcBatch is persistent");
+  CHECK(mpc.spec.literal_full_qp == 1, "default ConvexMpcBatch solves the literal 12N QP");
   qloco::A1MpcState st[2] = {};
   for (auto &s : st) {
     s.root_pos[2] = 0.30;

@@ -162,6 +162,10 @@ def lib():
         L.qo_srbd_persist_step.argtypes = [dp, C.POINTER(SrbdSpec), C.POINTER(AdmmSettings),
                                            fp, fp, fp, C.c_int, u8p, C.c_int, dp,
                                            C.POINTER(AdmmInfo)]
+        L.qo_srbd_persist_step_ex.restype = C.c_int
+        L.qo_srbd_persist_step_ex.argtypes = [dp, C.POINTER(SrbdSpec), C.POINTER(AdmmSettings),
+                                              fp, fp, fp, C.c_int, u8p, C.c_int, C.c_int, dp,
+                                              C.POINTER(AdmmInfo)]
         L.qo_a1_params_default.argtypes = [C.POINTER(A1Params)]
         L.qo_a1_qp_build.argtypes = [C.POINTER(A1Params), dp, u8p, dp, dp, dp, dp, dp, dp]
         L.qo_a1_compute_grf.restype = C.c_int
@@ -449,11 +453,14 @@ def persist_len(N):
 
 
 class PersistentMpc:
-    """The reference's member OSQP solver restated on the stance-only QP,
-    one record per controller."""
+    """The reference's member OSQP solver, one record per controller: on the
+    literal 12N-variable QP (literal=True: every call after the first is
+    OSQP's update path) or on the stance-only reduction (literal=False:
+    re-initialised when the stance set changes)."""
 
-    def __init__(self, N, **admm):
+    def __init__(self, N, literal=False, **admm):
         self.N = N
+        self.literal = int(bool(literal))
         self.sp = srbd_spec(N=N)
         self.st = admm_settings(**admm)
         self.rec = np.zeros(persist_len(N))
@@ -467,7 +474,7 @@ class PersistentMpc:
         ct = np.ascontiguousarray(ct, np.uint8)
         fps = int(ft.size == 12 * self.N and self.N > 1)
         cps = int(ct.size == 4 * self.N and self.N > 1)
-        lib().qo_srbd_persist_step(P(self.rec), C.byref(self.sp), C.byref(self.st),
-                                   P(x0, C.c_float), P(xr, C.c_float), P(ft, C.c_float), fps,
-                                   P(ct, C.c_uint8), cps, P(u), C.byref(info))
+        lib().qo_srbd_persist_step_ex(P(self.rec), C.byref(self.sp), C.byref(self.st),
+                                      P(x0, C.c_float), P(xr, C.c_float), P(ft, C.c_float), fps,
+                                      P(ct, C.c_uint8), cps, self.literal, P(u), C.byref(info))
         return u, info

@@ -127,11 +127,17 @@ def test_argument_validation_without_device_work():
     assert L.qloco_srbd_build(C.byref(bad), 4, *([None] * 10), None) == 4
     # missing required pointers
     assert L.qloco_srbd_solve(C.byref(sp), 4, *([None] * 10), None) == 100
-    # EiQuadProg limits (n <= 16, p <= 16, m <= 64)
-    assert L.qloco_max_gi_vars() == 16
+    # EiQuadProg limits: QPBaseClass's capacity (nVars <= 60, nIneq <= 300,
+    # QPBaseClass.h:49-51) rounded up -- n, p <= 64, m <= 320
+    assert L.qloco_max_gi_vars() == 64
+    lim = (C.c_int32 * 3)()
+    L.qloco_gi_limits(C.byref(lim, 0), C.byref(lim, 4), C.byref(lim, 8))
+    assert list(lim) == [64, 64, 320]
     args = [None, 0] * 6 + [None] * 4 + [None]
-    assert L.qloco_eiquadprog_solve(17, 0, 8, 1, *args) == 4
-    assert L.qloco_eiquadprog_solve(8, 0, 65, 1, *args) == 4
+    assert L.qloco_eiquadprog_solve(65, 0, 8, 1, *args) == 4
+    assert L.qloco_eiquadprog_solve(8, 65, 8, 1, *args) == 4
+    assert L.qloco_eiquadprog_solve(8, 0, 321, 1, *args) == 4
+    assert L.qloco_eiquadprog_solve(60, 10, 300, 1, *args) == 100  # in range: NULL pointers refused
     assert L.qloco_eiquadprog_solve(8, 0, 8, 0, *args) == 100  # NULL G even when empty
 
 

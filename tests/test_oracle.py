@@ -372,3 +372,40 @@ def test_persistent_solver_restatement_semantics():
             (cold_it if t == 0 else warm_it).append(info.iters)
             cold_it.append(Instance(sp, x0, xr, ft, ct).admm_reduced()[1].iters) if t else None
     assert np.mean(warm_it) < np.mean(cold_it)
+
+
+def test_persistent_literal_restatement_takes_update_path():
+    """oracle/persist.c with literal = 1 (the reference's 12N-variable QP):
+    the first call is exactly the cold full-QP solve (Instance.admm_full, bit
+    for bit); every later call -- phase switches included -- is OSQP's update
+    path: an identical repeat stops at the first check, and at a trot phase
+    switch the solve RESUMES (rho carried from the previous call instead of
+    the settings' 0.1; a re-initialisation would restart from 0.1) and needs
+    fewer iterations than a cold solve of the same instance."""
+    from cases import closed_loop_srbd
+    N, B = 10, 8
+    seq = closed_loop_srbd(N, B, 24, switch_every=6)
+    sp = O.srbd_spec(N=N)
+    switch_it, cold_it = [], []
+    for b in range(B):
+        pm = O.PersistentMpc(N, literal=True)
+        x0, xr, ft, ct = (a[b] for a in seq[0])
+        u1, i1 = pm.step(x0, xr, ft, ct)
+        xf, i_f = Instance(sp, x0, xr, ft, ct).admm_full()
+        assert i1.iters == i_f.iters and np.array_equal(u1, xf)
+        _, i2 = pm.step(x0, xr, ft, ct)
+        assert i2.iters == 25 and i2.status == 0
+        pm = O.PersistentMpc(N, literal=True)
+        for t, tick in enumerate(seq):
+            x0, xr, ft, ct = (a[b] for a in tick)
+            rho_before = pm.rec[100 * N]
+            u, info = pm.step(x0, xr, ft, ct)
+            assert info.status == 0
+            if t > 0 and not np.array_equal(ct, seq[t - 1][3][b]):
+                # the update path starts from the carried rho: with no further
+                # adaptation the final rho is the one the record held
+                if info.rho_updates == 0:
+                    assert info.rho_final == rho_before
+                switch_it.append(info.iters)
+                cold_it.append(Instance(sp, x0, xr, ft, ct).admm_full()[1].iters)
+    assert switch_it and np.mean(switch_it) < 0.7 * np.mean(cold_it), (switch_it, cold_it)

@@ -85,6 +85,40 @@ def test_eiquadprog_matches_restatement(n, p, m, zero_ce):
     assert exact >= 0.9 * ok, (exact, ok)
 
 
+@pytest.mark.parametrize("n,p,m,zero_ce", [(60, 10, 300, 3), (30, 0, 120, 0), (17, 17, 65, 4),
+                                           (64, 64, 320, 8), (40, 6, 200, 0)])
+def test_eiquadprog_wide_matches_restatement(n, p, m, zero_ce):
+    """The reference's QPBaseClass capacity (nVars <= 60, nIneq <= 300,
+    QPBaseClass.h:49-51) through qloco_eiquadprog_solve's size dispatch: one
+    QP per wavefront (qloco_gi_wide.hip), zero CE columns included (the
+    me = p / A(i) quirks).  Status and active-set iterations equal to the
+    restatement; x within 1e-9 relative (the triangular solves are column
+    sweeps, so results agree to rounding, not bit for bit), f within 1e-9."""
+    dev = _dev()
+    rng = np.random.default_rng(n * 1000 + p * 10 + m)
+    B = 24
+    probs = [random_qp(rng, n, p, m, zero_ce) for _ in range(B)]
+    stack = lambda k: np.stack([np.asfortranarray(pr[k]).ravel(order="F") for pr in probs])
+    res = qp.eiquadprog_solve(*(torch.from_numpy(stack(k)).to(dev) for k in range(6)),
+                              n=n, p=p, m=m)
+    torch.cuda.synchronize()
+    x = res["x"].cpu().numpy()
+    f = res["f"].cpu().numpy()
+    st = res["status"].cpu().numpy()
+    it = res["iters"].cpu().numpy()
+    solved = 0
+    for b in range(B):
+        xo, fo, sto, ito = oracle_eqp(*probs[b])
+        assert st[b] == sto, (b, st[b], sto)
+        assert it[b] == ito, (b, it[b], ito)
+        if sto == 0:
+            solved += 1
+            sc = max(1.0, np.abs(xo).max())
+            assert np.abs(x[b] - xo).max() <= 1e-9 * sc, (b, np.abs(x[b] - xo).max())
+            assert abs(f[b] - fo) <= 1e-9 * max(1.0, abs(fo)), (b, f[b], fo)
+    assert solved >= B // 2, solved
+
+
 def test_force_qp_matches_restatement_over_ticks():
     dev = _dev()
     rng = np.random.default_rng(7)

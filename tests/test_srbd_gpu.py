@@ -587,3 +587,140 @@ def test_srbd_wide_warm_and_persistent():
             assert dX <= 0.3, (t, b, dF, dM, dX)
             total += 1
     assert same >= 0.7 * total, (same, total)
+
+
+# --- the literal full QP (spec.literal_full_qp = 1): the reference's call as
+# written -- all 12N forces are ADMM variables, swing legs held by their
+# fz in [0, 0] rows (OSQP equality rows, rho_eq = 1e3 rho), Ruiz over the
+# full P and A (ConvexMpc.cpp:162-264, A1RobotControl.cpp:557-578).  Checked
+# against the oracle's fp64 OSQP-algorithm restatement of the SAME problem
+# (Instance.admm_full), at the reduced mode's bounds.
+
+@pytest.mark.parametrize("N,B,gait", [(10, 48, "trot"), (10, 24, "pace"), (10, 32, "mixed"),
+                                      (16, 12, "trot"), (20, 8, "pace"), (4, 16, "trot")])
+def test_srbd_literal_matches_full_restatement(N, B, gait):
+    """Literal mode vs Instance.admm_full (the reference's full 12N-variable
+    OSQP call, fp64): status OK, iterations within one check interval and
+    equal for >= 90 % (measured 0.97-1.0, tools/srbd_parity_scan.py
+    --literal, profiles/r3_literal_parity_scan.txt); where both stop at the
+    same check, predicted trajectory |dX|_Q <= 0.1 (measured max 0.031) and
+    per-step net wrench <= 15 N / 3 N m; where fp32 residuals pass one check
+    earlier or later the runs stop at different eps-optimal points (measured
+    |dX|_Q 0.1005, 77 N on one N = 10 pace instance of 48): |dX|_Q <= 0.3;
+    per-step net wrench <= 1 N / 0.1 N m for >= 90 % of instances at
+    N <= 10 (measured 0.94-0.98) and >= 85 % at N = 16 / 20 (192 / 240
+    fp32 variables: measured 0.875 / 0.917); objective within
+    5e-3 * max(1, |f*|) of the restatement's (measured p90 1.1e-5, max
+    2.9e-3 on the instance that stops a check early); swing forces within
+    the ADMM tolerance of zero (|f| <= 0.25 N); u0 = u[:12]."""
+    (x0, xr, ft, ct), r = _solve(N, B, gait, literal_full_qp=1)
+    sp = O.srbd_spec(N=N)
+    same = near = 0
+    for b in range(B):
+        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
+        xf, info = inst.admm_full()
+        assert r["status"][b] == 0 and info.status == 0, (b, r["status"][b], info.status)
+        assert abs(int(r["iters"][b]) - info.iters) <= 25, (b, r["iters"][b], info.iters)
+        u = r["u"][b].astype(np.float64)
+        du0, dF, dM, dX = _traj_metrics(u, xf, x0[b], xr[b], ft[b], ct[b], N)
+        if int(r["iters"][b]) == info.iters:
+            same += 1
+            assert dX <= 0.1, (b, dX)
+            assert dF <= 15.0 and dM <= 3.0, (b, dF, dM)
+        assert dX <= 0.3, (b, dX)
+        near += int(dF <= 1.0 and dM <= 0.1)
+        sc = max(1.0, abs(inst.exact_obj()))
+        assert abs(inst.obj(u) - inst.obj(xf)) <= 5e-3 * sc, (b, inst.obj(u), inst.obj(xf))
+        swing = np.repeat(ct[b] == 0, 3)
+        assert np.all(np.abs(u[swing]) <= 0.25), (b, np.abs(u[swing]).max())
+        assert np.array_equal(r["u0"][b], r["u"][b][:12])
+    assert same >= 0.9 * B, same
+    assert near >= (0.9 if N <= 10 else 0.85) * B, near
+
+
+def test_srbd_literal_edge_cases_and_modes():
+    """Literal mode corner cases: an all-swing instance (every fz row an
+    equality [0, 0]: the optimum is u = 0), an all-stance one and a
+    single-stance-step one in one N = 10 batch; the caller's max_stance_legs
+    is ignored (the literal problem always has 4N leg triples); warm_start = 1
+    resumes at the solution in <= 50 iterations."""
+    dev = _dev()
+    N, B = 10, 4
+    x0, xr, ft, ct = srbd.generate(SEED, N, B, "trot")
+    ct[0, :] = 0
+    ct[1, :] = 1
+    ct[2, 4:] = 0
+    args = [torch.from_numpy(a).to(dev) for a in (x0, xr, ft, ct)]
+    solver = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=1)
+    out = solver.solve(*args, full=True, max_legs=1)
+    torch.cuda.synchronize()
+    u = out.u.cpu().numpy().astype(np.float64)
+    st = out.status.cpu().numpy()
+    assert np.all(st == 0), st
+    assert np.abs(u[0]).max() <= 0.25, np.abs(u[0]).max()
+    sp = O.srbd_spec(N=N)
+    for b in range(B):
+        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
+        xf, info = inst.admm_full()
+        assert abs(int(out.iters[b]) - info.iters) <= 25
+        sc = max(1.0, abs(inst.exact_obj()))
+        assert abs(inst.obj(u[b]) - inst.obj(xf)) <= 1e-3 * sc, b
+    warm = torch.zeros((B, 32 * N), dtype=torch.float32, device=dev)
+    s = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=1, warm_start=1)
+    s.solve(*args, warm=warm)
+    second = s.solve(*args, warm=warm)
+    torch.cuda.synchronize()
+    assert np.all(second.iters.cpu().numpy() <= 50), second.iters.cpu().numpy()
+
+
+@pytest.mark.parametrize("N,B,T,every", [(10, 32, 24, 6), (16, 8, 12, 4)])
+def test_srbd_literal_persistent_closed_loop_matches_restatement(N, B, T, every):
+    """The reference's member OSQP solver over a trotting control loop
+    (A1RobotControl.cpp:556-578), on its literal QP: every controller flips
+    its trot phase each `every` MPC ticks (odd controllers half a period
+    later), and -- as in the reference, whose Hessian pattern never depends
+    on the contacts -- every call after the first takes OSQP's update path
+    (osqp_update_P / _lin_cost / _bounds: the fz rows re-typed, the adapted
+    rho and the scaled x, z, y carried).  Per tick, GPU (warm_start = 2,
+    literal_full_qp = 1) vs oracle/persist.c (qo_srbd_persist_step_ex,
+    literal = 1): status, iterations within one check interval and equal for
+    >= 85 % of (tick, controller) pairs, the carried rho within 10 % for
+    >= 90 % (an adaptation step changes rho by >= 5x; fp32 residual ratios
+    differ from fp64 at the 1e-3 level and compound over ticks: measured
+    0.92 at N = 16), and the trajectory-parity bounds on every solution.  Phase
+    switches resume rather than restart: the ticks after a switch need fewer
+    iterations than the cold first tick."""
+    from cases import closed_loop_srbd
+    dev = _dev()
+    seq = closed_loop_srbd(N, B, T, switch_every=every)
+    gpu = srbd.PersistentConvexMpc(B, dev, horizon=N, literal_full_qp=1)
+    orc = [O.PersistentMpc(N, literal=True) for _ in range(B)]
+    same = rho_ok = total = 0
+    it_first, it_switch = [], []
+    prev_ct = None
+    for t, (x0, xr, ft, ct) in enumerate(seq):
+        out = gpu.solve(*(torch.from_numpy(a).to(dev) for a in (x0, xr, ft, ct)), full=True)
+        torch.cuda.synchronize()
+        u = out.u.cpu().numpy()
+        st = out.status.cpu().numpy()
+        its = out.iters.cpu().numpy()
+        rec = gpu.record.cpu().numpy()
+        for b in range(B):
+            ub, info = orc[b].step(x0[b], xr[b], ft[b], ct[b])
+            assert st[b] == info.status == 0, (t, b, st[b], info.status)
+            assert abs(int(its[b]) - info.iters) <= 25, (t, b, its[b], info.iters)
+            same += int(its[b]) == info.iters
+            r64 = orc[b].rec[100 * N]
+            rho_ok += int(abs(rec[b, 100 * N] - r64) <= 0.1 * r64)
+            total += 1
+            _, dF, dM, dX = _traj_metrics(u[b], ub, x0[b], xr[b], ft[b], ct[b], N)
+            assert dX <= 0.1 and dF <= 15.0 and dM <= 3.0, (t, b, dF, dM, dX)
+            if t == 0:
+                it_first.append(int(its[b]))
+            elif not np.array_equal(ct[b], prev_ct[b]):
+                it_switch.append(int(its[b]))
+        prev_ct = ct
+    assert it_switch, "the sequence holds phase switches"
+    assert same >= 0.85 * total, (same, total)
+    assert rho_ok >= 0.9 * total, (rho_ok, total)
+    assert np.mean(it_switch) < np.mean(it_first)

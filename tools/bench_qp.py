@@ -33,6 +33,12 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 PEAK_FP64_TFLOPS = 78.6
+# algorithmic HBM bytes per robot: inputs com_des 3, leg_des 12, F_force_des 6,
+# rfoot / lfoot 3 + 3, base_p 3, feet_p 12, FT_total_des 6, y_coef 1 doubles
+# + mode, right_support int32 + the member state read (F_leg_ref, grf_opt: 24
+# doubles) = 592 B; outputs grf_opt, F_leg_guess, F_leg_ref (36 doubles) +
+# qp_solution, status, iters (int32) = 300 B
+ALG_BYTES = 592 + 300
 N, M = 12, 24
 
 
@@ -121,9 +127,9 @@ def main():
             "dtype": "f64", "data": "synthetic (tests/cases.force_inputs, seed 3)",
             "config": {"workload": "force QP, %d robots, modes 101/102/103, right_support 0/1/2" % B},
             "gi_iters_mean": float(iters.mean()), "status_ok_frac": float(np.mean(status == 0)),
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
+            "roofline": {"bound": "valu-fp64", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS,
-                         "traffic": _traffic(B),
+                         "traffic": _traffic(B), "alg_bytes": ALG_BYTES * B,
                          "note": "fp64 VALU (no MFMA on this path); algorithmic flops per solve "
                                  "in the tool docstring; latency-bound active set"}}
     if not args.no_cpu_baseline:

@@ -3,10 +3,11 @@
 // matrices with the W = 2 row layout (wave w, lane v: row 64w + v, 128
 // columns; column 63 and columns >= 64 + ncol1 are padding with a diagonal
 // only).  Reports max |K X - I| for each form and condition-number band.
-// Build: hipcc --offload-arch=gfx950 -O3 -DQLOCO_SRBD_MFMA_INV=1 -fno-slp-vectorize -mllvm
+// Build: hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -mllvm
 //   -pragma-unroll-threshold=200000 -I../../include -I../../quadrupedal_loco_amd/csrc
 //   w2_inverse.hip -o w2_inverse
 #include "qloco_srbd.hip"
+#include "srbd_mfma_inverse.inc"
 namespace qloco {
 void set_last_error(const char *, hipError_t) {}
 }  // probe: the C-ABI error slot lives in qloco_capi.hip
@@ -20,13 +21,14 @@ using namespace qloco;
 template <bool MF>
 __global__ __launch_bounds__(64) void inv1_kernel(const float *in, float *out, const int *ncols) {
   __shared__ __attribute__((aligned(16))) SrbdLds<1> S;
+  __shared__ __attribute__((aligned(16))) float sc[16 * 68];
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
   Row<1> K;
 #pragma unroll
   for (int c = 0; c < 64; ++c) K.k[c] = in[b * 16384 + t * 128 + c];
   if constexpr (MF) {
-    invert_w1_mfma(S, t, ncols[b], K);
+    invert_w1_mfma(sc, t, ncols[b], K);
   } else {
     invert_w1<false>(S, t, ncols[b], K);
   }
@@ -37,6 +39,7 @@ __global__ __launch_bounds__(64) void inv1_kernel(const float *in, float *out, c
 template <bool MF>
 __global__ __launch_bounds__(128) void inv_kernel(const float *in, float *out, const int *ncol1s) {
   __shared__ __attribute__((aligned(16))) SrbdLds<2> S;
+  __shared__ __attribute__((aligned(16))) float sc[2 * 8 * 256];
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
   Row<2> K;
@@ -44,7 +47,7 @@ __global__ __launch_bounds__(128) void inv_kernel(const float *in, float *out, c
   for (int c = 0; c < 128; ++c) K.k[c] = in[b * 16384 + t * 128 + c];
   const int n1 = ncol1s[b];
   if constexpr (MF) {
-    invert_w2_mfma(S, t, n1, K);
+    invert_w2_mfma(sc, t, n1, K);
   } else {
     const int ncol[2] = {63, n1};
     invert_w2(S, t, ncol, half2_chunks(n1), K);

@@ -1,7 +1,9 @@
 """Distribution of the SRBD parity quantities (GPU fp32 vs the oracle's fp64
 OSQP-algorithm ADMM restatement and vs the exact optimum of the literal QP),
 used to set the tolerances written in tests/test_srbd_gpu.py.
-    python tools/srbd_parity_scan.py [N B gait eps] ...   (GPU)
+    python tools/srbd_parity_scan.py [--literal] [N B gait eps] ...   (GPU)
+--literal: the literal 12N-variable mode (spec.literal_full_qp = 1) against
+the restatement of the same full QP (Instance.admm_full).
 Quantities per instance: |du0|, per-step net wrench (sum f, sum r x f),
 the predicted state trajectory X = Aqp x0 + Bqp u in the Q-norm, objective
 gap (f - f*) / max(1, |f*|), iterations."""
@@ -31,12 +33,12 @@ def metrics(inst, u, ref, x0, xr, ft, N, Bqp, q):
     return np.abs(u[:12] - ref[:12]).max(), dF, dM, dX
 
 
-def main(cases):
+def main(cases, literal=False):
     dev = torch.device("cuda:0")
     for N, B, gait, eps in cases:
         x0, xr, ft, ct = srbd.generate(20261015, N, B, gait)
         kw = dict(eps_abs=eps, eps_rel=eps, max_iter=20000) if eps != 1e-3 else {}
-        s = srbd.BatchedConvexMpc(horizon=N, **kw)
+        s = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=int(literal), **kw)
         out = s.solve(*(torch.from_numpy(a).to(dev) for a in (x0, xr, ft, ct)), full=True)
         torch.cuda.synchronize()
         u = out.u.cpu().numpy()
@@ -48,7 +50,8 @@ def main(cases):
         for b in range(B):
             inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
             Bqp = np_build(x0[b], xr[b], ft[b], ct[b], N)[6]
-            xa, info = inst.admm_reduced(eps_abs=eps, eps_rel=eps, max_iter=20000)
+            ref = inst.admm_full if literal else inst.admm_reduced
+            xa, info = ref(eps_abs=eps, eps_rel=eps, max_iter=20000)
             xe, _, _ = inst.exact()
             fe = inst.obj(xe)
             sc = max(1.0, abs(fe))
@@ -63,8 +66,11 @@ def main(cases):
         names = ["du0_adm", "dF_adm", "dM_adm", "dX_adm", "du0_ex", "dF_ex", "dM_ex", "dX_ex",
                  "du0_64ex", "dF_64ex", "dM_64ex", "dX_64ex", "gap_gpu", "gap_64", "gap_diff",
                  "dit", "status"]
-        print("== N=%d B=%d %s eps=%g  status counts %s" % (
-            N, B, gait, eps, dict(zip(*np.unique(st, return_counts=True)))))
+        print("== N=%d B=%d %s eps=%g%s  status counts %s  iters equal %.3f" % (
+            N, B, gait, eps, " literal" if literal else "",
+            dict(zip(*np.unique(st, return_counts=True))), float(np.mean(R[:, 15] == 0))))
+        near = np.mean((R[:, 1] <= 1.0) & (R[:, 2] <= 0.1))
+        print("  wrench <= 1 N / 0.1 N m: %.3f of instances" % near)
         for k, nm in enumerate(names[:-1]):
             v = R[:, k]
             print("  %-9s p50 %10.4g p90 %10.4g max %10.4g min %10.4g" % (
@@ -74,10 +80,13 @@ def main(cases):
 
 if __name__ == "__main__":
     a = sys.argv[1:]
+    lit = bool(a) and a[0] == "--literal"
+    if lit:
+        a = a[1:]
     if a:
         cases = [(int(a[i]), int(a[i + 1]), a[i + 2], float(a[i + 3])) for i in range(0, len(a), 4)]
     else:
         cases = [(10, 64, "trot", 1e-3), (10, 48, "mixed", 1e-3), (16, 24, "trot", 1e-3),
                  (20, 16, "pace", 1e-3), (10, 32, "trot", 1e-5), (10, 32, "trot", 1e-6),
                  (10, 24, "mixed", 1e-6), (20, 12, "pace", 1e-6)]
-    main(cases)
+    main(cases, lit)
