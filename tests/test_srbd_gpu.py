@@ -724,3 +724,79 @@ def test_srbd_literal_persistent_closed_loop_matches_restatement(N, B, T, every)
     assert same >= 0.85 * total, (same, total)
     assert rho_ok >= 0.9 * total, (rho_ok, total)
     assert np.mean(it_switch) < np.mean(it_first)
+
+
+# --- stream / graph behaviour of the class dispatch (its scratch is one set
+# per (device, caller stream), never freed while the process lives)
+
+def _three_class_batch(N=20):
+    parts = [srbd.generate(SEED, N, 6, g) for g in ("trot", "mixed", "stance")]
+    x0, xr, ft, ct = (np.concatenate([p[k] for p in parts]) for k in range(4))
+    ct[0:2, 4 * 5:] = 0  # one-wave class instances
+    return x0, xr, ft, ct
+
+
+def test_srbd_two_streams_mixed_classes():
+    """Two multi-class batches solved concurrently on two caller streams
+    (different batch sizes, so each stream's scratch is sized separately)
+    give bit-for-bit the results of one-at-a-time solves on the default
+    stream: no shared lists, counters or fork / join events."""
+    dev = _dev()
+    N = 20
+    a = _three_class_batch(N)
+    b = tuple(np.ascontiguousarray(np.concatenate([v, v[:5]])) for v in a)  # 23 instances
+    solver = srbd.BatchedConvexMpc(horizon=N)
+    ta = [torch.from_numpy(np.ascontiguousarray(v)).to(dev) for v in a]
+    tb = [torch.from_numpy(v).to(dev) for v in b]
+    ref_a = solver.solve(*ta, full=True)
+    ref_b = solver.solve(*tb, full=True)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    outs = []
+    for rep in range(3):
+        with torch.cuda.stream(s1):
+            oa = solver.solve(*ta, full=True, stream=s1.cuda_stream)
+        with torch.cuda.stream(s2):
+            ob = solver.solve(*tb, full=True, stream=s2.cuda_stream)
+        outs.append((oa, ob))
+    torch.cuda.synchronize()
+    for oa, ob in outs:
+        assert torch.equal(oa.u, ref_a.u) and torch.equal(oa.status, ref_a.status)
+        assert torch.equal(ob.u, ref_b.u) and torch.equal(ob.iters, ref_b.iters)
+
+
+def test_srbd_graph_capture_replay():
+    """The multi-class call captured into a HIP graph (after a warm-up call
+    on the capture stream sized its scratch) replays to the eager results;
+    a later, larger eager batch on that stream grows the scratch without
+    freeing the lists the graph reads, so a replay afterwards still matches."""
+    dev = _dev()
+    N = 20
+    x0, xr, ft, ct = _three_class_batch(N)
+    args = [torch.from_numpy(np.ascontiguousarray(v)).to(dev) for v in (x0, xr, ft, ct)]
+    solver = srbd.BatchedConvexMpc(horizon=N)
+    ref = solver.solve(*args, full=True)
+    torch.cuda.synchronize()
+    B = x0.shape[0]
+    out = solver.alloc_outputs(B, dev, full=True)
+    s = torch.cuda.Stream(dev)
+    legs = srbd.max_stance_legs(ct, N)
+    with torch.cuda.stream(s):
+        solver.solve(*args, out=out, max_legs=legs, stream=s.cuda_stream)  # warm-up: sizes the scratch
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        solver.solve(*args, out=out, max_legs=legs, stream=s.cuda_stream)
+    for k in range(2):
+        out.u.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out.u, ref.u) and torch.equal(out.status, ref.status)
+    big = [torch.cat([t] * 300) for t in args]  # 5400 instances: the scratch grows
+    with torch.cuda.stream(s):
+        solver.solve(*big, max_legs=legs, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    out.u.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out.u, ref.u)
