@@ -53,6 +53,16 @@ namespace qloco {
 
 constexpr int kMaxN = 20;    // max horizon compiled in (BASELINE configs: N <= 20)
 constexpr int kLegsPerWave = 21;
+// The one-wave class takes instances of at most kW1Legs stance legs.  20
+// (60 variables, every Go1 trot / pace N = 10 instance) lets the one-wave
+// kernel carry a single 60-column form of its inverse, matvec and Ruiz
+// sweeps -- 124 -> ~80 KB of code; 21-leg instances then go to the two-wave
+// class.  21 keeps the 64-column forms as well.
+#ifndef QLOCO_W1_LEGS
+#define QLOCO_W1_LEGS 20
+#endif
+constexpr int kW1Legs = QLOCO_W1_LEGS;
+static_assert(kW1Legs == 20 || kW1Legs == 21, "one-wave class: 20 or 21 legs");
 
 struct SrbdArgs {
   int N, feet_per_step, contacts_per_step, output_frame;
@@ -491,51 +501,52 @@ __device__ __forceinline__ float finalize_row(const SrbdLds<W> &S, int t, int cb
 }
 
 // In-place Gauss-Jordan inverse of the register-resident SPD K (no
-// pivoting; Ruiz-scaled, so pivots are O(1)).  The pivot row k is broadcast
-// with entry k replaced by p+1.  With g = A_rk / p (g = 1 - 1/p on the
-// pivot lane) ONE shared update
-//   A_rc <- A_rc - g * bcast_c
-// performs the whole GJ step, column k included (non-pivot:
-// A_rk - g(p+1) = -g; pivot: p - (1-1/p)(p+1) = 1/p).  GJ on a symmetric
-// matrix keeps A_kc = +A_ck for unprocessed c and -A_ck for processed
-// c (< k), so for W = 1 every lane writes its own column-k entry (a static
-// register: the pivot loop is unrolled) and the pivot is a v_readlane --
-// one coalesced ds_write_b32 and one ds_read_b128 per pivot, the row fanned
-// out by DPP.  Only the valid pivots run; padding rows / columns are the
-// identity and never change.
+// pivoting; Ruiz-scaled).  Step k: every row r takes
+//   A_rc <- A_rc - g_r * (pivot row)_c,  g_r = A_rk / p   (one DPP FMA per column)
+// with the pivot row's own scaling by 1/p folded into the same FMA
+// (g_k = 1 - 1/p against the row plus the identity, e_k = p + 1).  That fused
+// form rounds 1 - 1/p and carries a relative error ~p*eps into column k, so
+// for a large pivot (p > kGjExactPivot) column k is then written exactly
+// (A_kk = 1/p, A_rk = -g_r): the literal QP's equality rows (rho_eq = 1e3 rho)
+// reach p ~ 3e5, where the fused column was 1e3x off and ADMM diverged
+// (DESIGN.md §3e).  Small pivots keep the fused column, whose rounding is
+// shared with the pivot row (measured the more accurate at eps 1e-6).  GJ on a
+// symmetric matrix keeps A_kc = +A_ck for unprocessed c and -A_ck for
+// processed c (< k), so every lane writes its own column-k entry as the pivot
+// row (a static register: the pivot loop is unrolled) and the pivot is a
+// v_readlane -- one coalesced ds_write_b32 and one ds_read_b128 per pivot,
+// the row fanned out by DPP.  Only the valid pivots run; padding rows /
+// columns are the identity and never change.
+constexpr float kGjExactPivot = 16.0f;
+
 template <bool C60>
 __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1> &K) {
   const int lane = t & 63;
   int nc = __builtin_amdgcn_readfirstlane(ncol);
+  // pivots emitted: 60 when the one-wave class stops at 20 legs (code size)
+  constexpr int KP = (C60 && kW1Legs <= 20) ? 60 : 64;
 #pragma unroll
-  for (int k = 0; k < 64; ++k) {
+  for (int k = 0; k < KP; ++k) {
     asm volatile("" : "+s"(nc));  // the per-pivot compare stays a scalar one (not 64 hoisted masks)
     if (k >= nc) continue;  // wave-uniform; the loop stays fully unrolled (static register k)
     const int buf = k & 1;
     float *bcf = reinterpret_cast<float *>(&S.bc[buf][0]);
     int tt = t;
     asm volatile("" : "+v"(tt));  // per-pivot compares stay local (no 64 hoisted masks)
-    const float v = K.k[k];  // A_tk
+    const float v = K.k[k];
     const float p = __builtin_bit_cast(
         float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
-    float e = (tt < k) ? -v : v;
-    e = (tt == k) ? p + 1.0f : e;
-    bcf[tt] = e;
+    bcf[tt] = (tt == k) ? p + 1.0f : ((tt < k) ? -v : v);
     bsync<1>();
     const f4v r0 = S.bc[buf][lane & 15];
     const float pinv = __builtin_amdgcn_rcpf(p);
-    const float g = (tt == k) ? (1.0f - pinv) : v * pinv;
-    const float ng = -g;
+    const float ng = -((tt == k) ? (1.0f - pinv) : v * pinv);
     if constexpr (C60) {
       QL_DPP_GJ60(K.k, 0, r0, ng);
     } else {
       QL_DPP_GJ64(K.k, 0, r0, ng);
     }
-    // column k exactly: the fused update forms it by cancellation
-    // (p - (1 - 1/p)(p + 1), A_rk - (A_rk / p)(p + 1)), whose absolute error
-    // ~ p * ulp swamps 1/p once p is large (a literal-QP equality row at
-    // rho_eq = 1e3 rho: measured K^-1 diagonal 1e3x off at rho = 290)
-    K.k[k] = (tt == k) ? pinv : ng;
+    if (p > kGjExactPivot) K.k[k] = (tt == k) ? pinv : ng;  // column k exactly
   }
   bsync<1>();
 }
@@ -570,21 +581,18 @@ __device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, int
     float *bcf = reinterpret_cast<float *>(&S.bc[buf][0]);
     int tt = t;
     asm volatile("" : "+v"(tt));
-    const float v = K.k[k];  // A_tk
-    float e = (tt < k) ? -v : v;
-    e = (tt == k) ? v + 1.0f : e;
-    bcf[tt] = e;
+    const float v = K.k[k];
+    bcf[tt] = (tt == k) ? v + 1.0f : ((tt < k) ? -v : v);
     S.colv[buf][tt] = v;  // the pivot A_kk for the other wave (no divergent store)
     __syncthreads();
     const float p = S.colv[buf][k];
     const f4v r0 = S.bc[buf][lane & 15], r1 = S.bc[buf][16 + (lane & 15)];
     const float pinv = __builtin_amdgcn_rcpf(p);
-    const float g = (tt == k) ? (1.0f - pinv) : v * pinv;
-    const float ng = -g;
+    const float ng = -((tt == k) ? (1.0f - pinv) : v * pinv);
     QL_DPP_GJ64(K.k, 0, r0, ng);
     (void)c2;  // one form: per-bucket forms triple the (instruction-cache bound) code
     QL_DPP_GJ64(K.k, 64, r1, ng);
-    K.k[k] = (tt == k) ? pinv : ng;  // column k exactly (see invert_w1)
+    if (p > kGjExactPivot) K.k[k] = (tt == k) ? pinv : ng;  // column k exactly (invert_w1)
   }
 }
 
@@ -696,7 +704,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
   const int nlegs = uni(S.nlegs);
   const int n = 3 * nlegs;
   if (nlegs < a.leg_lo || nlegs > a.leg_hi) return;  // the other launch's instance
-  if (nlegs > kLegsPerWave * W) {  // uniform: the caller's max_stance_legs was too small
+  if (nlegs > (W == 1 ? kW1Legs : kLegsPerWave * W)) {  // uniform: the caller's max_stance_legs was too small
     if (t < 12) a.u0[b * 12 + t] = NAN;
     if (a.u)
       for (int k = t; k < 12 * N; k += NC) a.u[b * 12 * N + k] = NAN;
@@ -732,7 +740,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
     ncol[w] = 3 * lw;
   }
   // every valid column below 60: the 60-column DPP forms (uniform)
-  const bool c60 = W == 1 && __builtin_amdgcn_readfirstlane(ncol[0]) <= 60;
+  const bool c60 = W == 1 && (kW1Legs <= 20 || __builtin_amdgcn_readfirstlane(ncol[0]) <= 60);
   const int c2 = W == 2 ? half2_chunks(__builtin_amdgcn_readfirstlane(ncol[W - 1])) : 16;
   const int lslot = lane / 3;
   const int comp = lane - 3 * lslot;
@@ -889,7 +897,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
                            : (a.adaptive_rho ? a.rho_interval : 0);
   int status = QLOCO_MAX_ITER, iter = 0;
   float px = 0.0f;  // scaled (P x)_v of the last residual evaluation
-  bool have_px = false;
   bool first = true;
   int rho_updates = 0;
 
@@ -942,17 +949,17 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
     }
   };
 
-  // P row (closed form) and Ruiz equilibration, once
-  {
-    const PCoef pc = p_coef<W>(S, lo, hi, comp, valid, dtm, dt2m);
-    gen_p_row<W>(S, pc, t, valid, step, comp, r2v, K);
-#ifdef QLOCO_ABLATE_DUP_GENP  // timing experiments only (tools/variant_lib.py)
-    asm volatile("" ::: "memory");
-    gen_p_row<W>(S, pc, t, valid, step, comp, r2v, K);
-#endif
-  }
-  {
-    {
+  // One code path for the first factorisation and every adaptive-rho
+  // refactorisation: closed-form P row -> (first: Ruiz) -> K = cs D P D +
+  // leg blocks -> K^-1 -> ADMM blocks.  Each piece is emitted once (the
+  // kernel is instruction-cache bound: DESIGN.md §3d).
+  for (;;) {
+    {  // closed-form P row, regenerated for every factorisation
+      const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
+      const PCoef pc = p_coef<W>(S, blo, bhi, comp, valid, dtm, dt2m);
+      gen_p_row<W>(S, pc, t, valid, (int)bhi.z, comp, S.aux[0][t], K);
+    }
+    if (first) {
       QL_PHASE(3);
       // ---------------- 7. modified Ruiz equilibration (OSQP scaling.c); K
       // keeps the unscaled P, row norms of the scaled P = cs D P D come from
@@ -1041,10 +1048,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
       bsync<W>();
       QL_PHASE(4);
     }
-  }
-  // One code path for the first factorisation and every adaptive-rho
-  // refactorisation: K = cs D P D + leg blocks -> K^-1 -> ADMM blocks.
-  for (;;) {
     // ---------------- 8. K = cs D P D + sigma I + A' rho A, inverse in registers
     {
       float add0, add1, add2;
@@ -1126,8 +1129,11 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
     bool refactor = false;
 
     // Iterations run in event-free blocks up to the next termination check,
-    // adaptive-rho point or max_iter, so the hot loop carries no modulo tests.
-    while (iter < a.max_iter) {
+    // adaptive-rho point or max_iter, so the hot loop carries no modulo tests;
+    // the residual evaluation after a block is the only one in the kernel
+    // (checks, rho estimates and the final max_iter status share it).
+    for (;;) {
+      if (iter < a.max_iter) {
       int next = a.max_iter;
       if (ctm) next = min(next, (iter / ctm + 1) * ctm);
       if (interval) next = min(next, (iter / interval + 1) * interval);
@@ -1247,59 +1253,54 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
           run_block(std::false_type{}, std::integral_constant<int, 16>{});
         }
       }
-      const bool can_check = ctm && (iter % ctm == 0);
-      const bool do_rho = interval && (iter % interval == 0);
-      if (can_check || do_rho) {
-        float o[6], r[6];
-        residuals(o, r, do_rho);
-        have_px = true;
-        const float pri_res = o[0], dua_res = cinv * o[3];
-        if (can_check) {
-          const float eps_p = a.eps_abs + a.eps_rel * fmaxf(o[1], o[2]);
-          const float eps_d = a.eps_abs + a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
-          if (pri_res < eps_p && dua_res < eps_d) {
-            status = QLOCO_OK;
-            break;
-          }
+      }
+      // OSQP: termination check every check_termination iterations, rho
+      // adaptation every interval; past max_iter the status is "solved
+      // inaccurate" or "max_iter reached" from the same residuals (an
+      // adaptation at the last iteration keeps its rho for the record, its
+      // refactorisation would be dead work and is skipped)
+      const bool fin = iter >= a.max_iter;
+      const bool can_check = ctm && iter > 0 && (iter % ctm == 0);
+      const bool do_rho = interval && iter > 0 && (iter % interval == 0);
+      if (!(can_check || do_rho || fin)) continue;
+      float o[6], r[6];
+      residuals(o, r, do_rho);
+      const float pri_res = o[0], dua_res = cinv * o[3];
+      if (can_check) {
+        const float eps_p = a.eps_abs + a.eps_rel * fmaxf(o[1], o[2]);
+        const float eps_d = a.eps_abs + a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
+        if (pri_res < eps_p && dua_res < eps_d) {
+          status = QLOCO_OK;
+          break;
         }
-        if (do_rho) {  // compute_rho_estimate + adapt_rho
-          const float pn = r[0] / (fmaxf(r[1], r[2]) + 1e-30f);
-          const float dn = r[3] / (fmaxf(fmaxf(qn[1], r[4]), r[5]) + 1e-30f);
-          float rho_new = rho * sqrtf(pn / (dn + 1e-30f));
-          rho_new = fminf(fmaxf(rho_new, 1e-6f), 1e6f);
-          if (rho_new > rho * a.rho_tol || rho_new < rho / a.rho_tol) {
-            rho = rho_new;
-            rvi = 1.0f / rho;
-            rho_updates++;
+      }
+      if (do_rho) {  // compute_rho_estimate + adapt_rho
+        const float pn = r[0] / (fmaxf(r[1], r[2]) + 1e-30f);
+        const float dn = r[3] / (fmaxf(fmaxf(qn[1], r[4]), r[5]) + 1e-30f);
+        float rho_new = rho * sqrtf(pn / (dn + 1e-30f));
+        rho_new = fminf(fmaxf(rho_new, 1e-6f), 1e6f);
+        if (rho_new > rho * a.rho_tol || rho_new < rho / a.rho_tol) {
+          rho = rho_new;
+          rvi = 1.0f / rho;
+          rho_updates++;
+          if (!fin) {
             refactor = true;
             break;
           }
         }
       }
+      if (fin) {  // max_iter reached (OSQP: solved inaccurate or max_iter)
+        const float ep = 10.f * a.eps_abs + 10.f * a.eps_rel * fmaxf(o[1], o[2]);
+        const float ed = 10.f * a.eps_abs + 10.f * a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
+        status = (pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE : QLOCO_MAX_ITER;
+        break;
+      }
     }
     if (!refactor) break;
-    {
-      const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
-      const PCoef pc = p_coef<W>(S, blo, bhi, comp, valid, dtm, dt2m);
-      gen_p_row<W>(S, pc, t, valid, (int)bhi.z, comp, S.aux[0][t], K);
-    }
-  }
-  if (status != QLOCO_OK) {  // max_iter reached (OSQP: solved inaccurate or max_iter)
-    float o[6], r[6];
-    residuals(o, r, false);
-    have_px = true;
-    const float pri_res = o[0], dua_res = cinv * o[3];
-    const float ep = 10.f * a.eps_abs + 10.f * a.eps_rel * fmaxf(o[1], o[2]);
-    const float ed = 10.f * a.eps_abs + 10.f * a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
-    status = (pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE : QLOCO_MAX_ITER;
   }
 
   QL_PHASE(7);
   // ---------------- 10. outputs: unscale, objective, scatter to leg slots
-  if (!have_px) {  // max_iter == 0
-    float o[6], r[6];
-    residuals(o, r, false);
-  }
   const float Dr_o = S.Dc[t];
   const int pr_o = S.pair[t];
   const int step_o = pr_o >> 2, leg_o = pr_o & 3;
@@ -1409,7 +1410,7 @@ __global__ __launch_bounds__(256) void srbd_classify_kernel(const SrbdArgs a, in
       for (int k = 0; k < 4; ++k) legs += a.contacts[b * 4 + k] != 0;
       legs *= N;
     }
-    cls = legs <= kLegsPerWave ? 0 : (legs <= 2 * kLegsPerWave ? 1 : 2);
+    cls = legs <= kW1Legs ? 0 : (legs <= 2 * kLegsPerWave ? 1 : 2);
     cls = cls > top ? top : cls;
   }
   const int lane = threadIdx.x & 63;
@@ -1640,9 +1641,11 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
         hipLaunchKernelGGL((srbd_admm_big_kernel<false>), grid, dim3(kBigThreads), 0, s, a);
     }
   };
-  const int top = legs <= kLegsPerWave ? 0 : (legs <= 2 * kLegsPerWave ? 1 : 2);
-  if (top == 0) {
-    launch(0, st);
+  const int top = legs <= kW1Legs ? 0 : (legs <= 2 * kLegsPerWave ? 1 : 2);
+  if (top == 0 || a.literal) {
+    // one class: every instance of the literal QP has 4N leg triples, so no
+    // classification and no empty class launches
+    launch(top, st);
   } else {
     std::lock_guard<std::mutex> lk(g_srbd_scratch_mu);
     SrbdScratch *sc = nullptr;

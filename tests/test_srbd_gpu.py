@@ -72,7 +72,7 @@ def _solve(N, B, gait, first=0, **spec):
 
 
 @pytest.mark.parametrize("N,B,gait", [(10, 48, "trot"), (10, 24, "pace"), (10, 32, "mixed"),
-                                      (16, 12, "trot"), (20, 8, "pace"), (4, 16, "stance")])
+                                      (16, 12, "trot"), (20, 16, "pace"), (4, 16, "stance")])
 def test_srbd_matches_admm_restatement(N, B, gait):
     (x0, xr, ft, ct), r = _solve(N, B, gait)
     sp = O.srbd_spec(N=N)

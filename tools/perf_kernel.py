@@ -34,7 +34,10 @@ x0, xr, ft, ct = srbd.generate(20261015, N, B, GAIT)
 dev = torch.device("cuda:0")
 args = [torch.from_numpy(a).to(dev) for a in (x0, xr, ft, ct)]
 legs = srbd.max_stance_legs(ct, N)
-s = srbd.BatchedConvexMpc(horizon=N, **VARIANTS[name])
+LIT = int(os.environ.get("LITERAL", 0))  # 1: the literal 12N-variable QP
+if LIT:
+    legs = 4 * N
+s = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=LIT, **VARIANTS[name])
 out = s.alloc_outputs(B, dev)
 for _ in range(2):
     s.solve(*args, out=out, max_legs=legs)
@@ -46,7 +49,8 @@ for _ in range(reps):
 e1.record()
 torch.cuda.synchronize()
 it = out.iters.float()
-print("%-10s %-6s N=%-2d %-8s B=%6d  %9.1f us/launch  iters mean %.1f p99 %d max %d  rho_updates mean %.2f max %d" % (
-    os.path.basename(os.path.dirname(os.environ.get("QLOCO_LIB", "/prod/x"))), GAIT, N, name, B,
+print("%-10s %-6s%s N=%-2d %-8s B=%6d  %9.1f us/launch  iters mean %.1f p99 %d max %d  rho_updates mean %.2f max %d" % (
+    os.path.basename(os.path.dirname(os.environ.get("QLOCO_LIB", "/prod/x"))), GAIT,
+    " lit" if LIT else "", N, name, B,
     e0.elapsed_time(e1) / reps * 1e3, it.mean().item(), int(it.quantile(0.99).item()), int(it.max().item()),
     out.rho_updates.float().mean().item(), int(out.rho_updates.max().item())), flush=True)

@@ -10,6 +10,9 @@ import sys
 
 
 def summarise(d, kern):
+    """{kernel name: {counter: mean over that kernel's dispatches}} for the
+    kernels whose name contains `kern` (one entry per distinct kernel, so the
+    classes of a multi-class SRBD batch are not averaged together)."""
     dbs = glob.glob(os.path.join(d, "**", "*.db"), recursive=True)
     if not dbs:
         return None
@@ -17,19 +20,22 @@ def summarise(d, kern):
     rows = cur.execute("select dispatch_id, kernel_name, counter_name, value, duration "
                        "from counters_collection").fetchall()
     per = collections.defaultdict(float)
-    dur = {}
+    dur = collections.defaultdict(dict)
     for disp, k, c, v, du in rows:
         if kern in str(k):
-            per[(disp, c)] += v
-            dur[disp] = du
-    agg = collections.defaultdict(list)
-    for (disp, c), v in per.items():
-        agg[c].append(v)
-    out = {c: sum(v) / len(v) for c, v in sorted(agg.items())}
-    if dur:
-        out["duration_ns"] = sum(dur.values()) / len(dur)
-        out["dispatches"] = len(dur)
-    return out
+            per[(str(k), disp, c)] += v
+            dur[str(k)][disp] = du
+    res = {}
+    for name in sorted(dur):
+        agg = collections.defaultdict(list)
+        for (k, disp, c), v in per.items():
+            if k == name:
+                agg[c].append(v)
+        out = {c: sum(v) / len(v) for c, v in sorted(agg.items())}
+        out["duration_ns"] = sum(dur[name].values()) / len(dur[name])
+        out["dispatches"] = len(dur[name])
+        res[name] = out
+    return res
 
 
 if __name__ == "__main__":
@@ -40,5 +46,5 @@ if __name__ == "__main__":
         sorted(glob.glob(os.path.join(root, "pmc*")))
     for d in dirs:
         s = summarise(d, kern)
-        if s:
-            print(os.path.basename(d), {k: round(v) for k, v in s.items()})
+        for name, v in (s or {}).items():
+            print(os.path.basename(d), name[:60], {k: round(x) for k, x in v.items()})
