@@ -103,15 +103,18 @@ struct Row {
 };
 #define KE(K, c) ((K).k[(c)])
 
-template <int W>
+// NM: the largest horizon the instantiation admits (per-step tables are
+// sized by it: NM = 10 keeps the one-wave workgroup under 10 KB of LDS, so
+// 16 fit a CU -- four waves per SIMD)
+template <int W, int NM = kMaxN>
 struct SrbdLds {
   static constexpr int NC = 64 * W;
   f4v bc[2][NC / 4];       // broadcast ring (KKT rhs, GJ pivot rows, Ruiz D)
   f4v bv[NC][2];           // per var: {b0,b1,b2,e0}, {e1,e2,step,comp}
   float xs[NC];            // unscaled x per var (P x)
   float Dc[NC];            // Ruiz column scaling D
-  float err[12 * kMaxN];   // per-step row values (gradient error / aggregates)
-  float Wc[12 * kMaxN];    // per-step Bqp' weights: rows 0..5 W1, rows 6..11 W0
+  float err[12 * NM];   // per-step row values (gradient error / aggregates)
+  float Wc[12 * NM];    // per-step Bqp' weights: rows 0..5 W1, rows 6..11 W0
   float q2[16];
   float r2[12];
   float x0[16];
@@ -120,15 +123,15 @@ struct SrbdLds {
   f4v arz[NC];              // per var: scaled A entries (ra0, ra1, rz0, rz1) of its 2 slots
   float qs[NC];             // per var: scaled q
   int pair[NC];             // per var: 4*step + leg
-  int cst[NC];              // per var: step, kMaxN on padding (row of zeros in k0k2)
-  f2v k0k2[kMaxN * (kMaxN + 1)];  // [row step][col step]: horizon sums K0, K2
+  int cst[NC];              // per var: step, NM on padding (row of zeros in k0k2)
+  f2v k0k2[NM * (NM + 1)];  // [row step][col step]: horizon sums K0, K2
   float piv[2];
   float colv[W == 1 ? 1 : 2][W == 1 ? 1 : NC];  // W = 2 inverse: pivot column
   float red[W][16];
-  int legtab[4 * kMaxN];   // stance pair -> 4*step + leg
-  int stepstart[kMaxN + 1];
+  int legtab[4 * NM];   // stance pair -> 4*step + leg
+  int stepstart[NM + 1];
   int nlegs;
-  uint8_t ct[4 * kMaxN];
+  uint8_t ct[4 * NM];
 };
 
 // LDS ordering between the lanes of ONE wave needs no s_barrier (a wave's
@@ -229,8 +232,8 @@ __device__ __forceinline__ float bsum(float v, float (*red)[16]) {
 }
 
 // (Bqp' w)_v for a variable of step `step`, component `comp`, from S.Wc.
-template <int W>
-__device__ __forceinline__ float bqp_t(const SrbdLds<W> &S, int step, int comp, f4v lo, f4v hi,
+template <int W, int NM>
+__device__ __forceinline__ float bqp_t(const SrbdLds<W, NM> &S, int step, int comp, f4v lo, f4v hi,
                                        float dtm, float dt2m) {
   const float *w = S.Wc + 12 * step;
   float acc = lo.x * w[6] + lo.y * w[7] + lo.z * w[8];
@@ -246,22 +249,22 @@ __device__ __forceinline__ float bqp_t(const SrbdLds<W> &S, int step, int comp, 
 //      on b rows (6..11), sum_{j<i} (i-j) agg_j on e rows (0..5);
 //  suffix: S.Wc[j][r] = sum_{i>=j} wt(i-j) S.err[i][r]; wt = 1 on b rows
 //      (W0), (i-j) on e rows (W1).
-template <int W>
-__device__ __forceinline__ void row_scans(SrbdLds<W> &S, int N, bool forward) {
+template <int W, int NM>
+__device__ __forceinline__ void row_scans(SrbdLds<W, NM> &S, int N, bool forward) {
   const int r = threadIdx.x;
 #ifdef QLOCO_ABLATE_NO_SCAN  // timing experiments only
   if (forward) return;
 #endif
   if (r >= 12) return;
   const bool brow = r >= 6;
-  float v[kMaxN];
+  float v[NM];
 #pragma unroll
-  for (int i = 0; i < kMaxN; ++i) v[i] = S.err[12 * i + r];
+  for (int i = 0; i < NM; ++i) v[i] = S.err[12 * i + r];
   if (forward) {
     const float q = S.q2[r];
     float pa = 0.0f, pe = 0.0f, se = 0.0f;
 #pragma unroll
-    for (int i = 0; i < kMaxN; ++i) {
+    for (int i = 0; i < NM; ++i) {
       if (i < N) {
         se += pe;
         pe += v[i];
@@ -272,7 +275,7 @@ __device__ __forceinline__ void row_scans(SrbdLds<W> &S, int N, bool forward) {
   }
   float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
-  for (int j = kMaxN - 1; j >= 0; --j) {
+  for (int j = NM - 1; j >= 0; --j) {
     if (j < N) {
       s1 += s0;  // S1[j] = S1[j+1] + S0[j+1]
       s0 += v[j];
@@ -287,13 +290,13 @@ __device__ __forceinline__ void row_scans(SrbdLds<W> &S, int N, bool forward) {
 // (sum_{i >= max(j,k)} 1 and sum_{i >= max(j,k)} (i-j)(i-k)).  All lanes, 12N
 // outputs, the table row and the aggregates read up front when NB (= N) is
 // a compile-time constant (N = 10); other horizons use rolled loops.
-template <int W, int NB>
-__device__ __forceinline__ void horizon_rows(SrbdLds<W> &S, int N) {
+template <int W, int NB, int NM>
+__device__ __forceinline__ void horizon_rows(SrbdLds<W, NM> &S, int N) {
   constexpr int NT = 64 * W;
   if constexpr (NB == 0) {  // any horizon: rolled loops (cold configurations)
     for (int idx = threadIdx.x; idx < 12 * N; idx += NT) {
       const int j = idx / 12, r = idx - 12 * j;
-      const f2v *kr = &S.k0k2[j * (kMaxN + 1)];
+      const f2v *kr = &S.k0k2[j * (NM + 1)];
       float acc = 0.0f;
       for (int k = 0; k < N; ++k) acc = fmaf(r >= 6 ? kr[k].x : kr[k].y, S.err[12 * k + r], acc);
       S.Wc[idx] = S.q2[r] * acc;
@@ -305,7 +308,7 @@ __device__ __forceinline__ void horizon_rows(SrbdLds<W> &S, int N) {
     const int idx = threadIdx.x + NT * pass;
     if (idx < 12 * N) {
       const int j = idx / 12, r = idx - 12 * j;
-      const f2v *kr = &S.k0k2[j * (kMaxN + 1)];
+      const f2v *kr = &S.k0k2[j * (NM + 1)];
       float a0 = 0.0f, a1 = 0.0f;
       if (r >= 6) {
 #pragma unroll
@@ -331,8 +334,8 @@ __device__ __forceinline__ void horizon_rows(SrbdLds<W> &S, int N) {
 //  (b) state rows s_i (b rows: prefix sum, e rows: weighted prefix sum),
 //      w_i = Q s_i, suffix weights W0 / W1 per (j, r) -> S.Wc (horizon_rows)
 //  (c) this lane's (Bqp' w)_v + R x_v
-template <int W>
-__device__ __forceinline__ float p_times_x(SrbdLds<W> &S, int N, bool valid, int step, int comp,
+template <int W, int NM>
+__device__ __forceinline__ float p_times_x(SrbdLds<W, NM> &S, int N, bool valid, int step, int comp,
                                            f4v lo, f4v hi, float r2v, float xu, float dtm,
                                            float dt2m) {
   const int t = threadIdx.x;
@@ -390,8 +393,8 @@ __device__ __forceinline__ void k0k2(float ja, float jb, float Nf, float &K0, fl
 struct PCoef {
   float bq0, bq1, bq2, eq0, eq1, eq2, linb, line;
 };
-template <int W>
-__device__ __forceinline__ PCoef p_coef(const SrbdLds<W> &S, f4v lo, f4v hi, int comp, bool valid,
+template <int W, int NM>
+__device__ __forceinline__ PCoef p_coef(const SrbdLds<W, NM> &S, f4v lo, f4v hi, int comp, bool valid,
                                         float dtm, float dt2m) {
   PCoef c;
   c.bq0 = S.q2[6] * lo.x;
@@ -409,11 +412,11 @@ __device__ __forceinline__ PCoef p_coef(const SrbdLds<W> &S, f4v lo, f4v hi, int
 // come in leg triples (lanes 3l..3l+2 of a wave, lane 63 padding), so the
 // column component is static and K0 / K2 -- functions of the row and column
 // steps only -- are one LDS table read per triple.
-template <int W>
-__device__ __forceinline__ void gen_p_row(const SrbdLds<W> &S, const PCoef &pc, int t, bool valid,
+template <int W, int NM>
+__device__ __forceinline__ void gen_p_row(const SrbdLds<W, NM> &S, const PCoef &pc, int t, bool valid,
                                           int step, int comp, float r2v, Row<W> &K) {
   // opaque copies: keep LICM from hoisting per-column selects out of the ADMM loop
-  int tt = t, kb = step * (kMaxN + 1);
+  int tt = t, kb = step * (NM + 1);
   // padding lanes have zero coefficients, so only their diagonal needs a 1
   float dadd = valid ? r2v : 1.0f;
   float lb0 = comp == 0 ? pc.linb : 0.0f, lb1 = comp == 1 ? pc.linb : 0.0f,
@@ -468,8 +471,8 @@ __device__ __forceinline__ int half2_chunks(int ncol1) {
 // touching only the lane's own leg columns (static column -> leg map; D_c
 // fanned out from one LDS chunk per lane by DPP).  Returns the diagonal
 // (pivot tracking of the W = 2 inverse).
-template <int W>
-__device__ __forceinline__ float finalize_row(const SrbdLds<W> &S, int t, int cbase, float rs,
+template <int W, int NM>
+__device__ __forceinline__ float finalize_row(const SrbdLds<W, NM> &S, int t, int cbase, float rs,
                                               float add0, float add1, float add2, bool c60,
                                               int c2, Row<W> &K) {
   constexpr int NC = 64 * W;
@@ -519,8 +522,8 @@ __device__ __forceinline__ float finalize_row(const SrbdLds<W> &S, int t, int cb
 // columns are the identity and never change.
 constexpr float kGjExactPivot = 16.0f;
 
-template <bool C60>
-__device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1> &K) {
+template <bool C60, int NM>
+__device__ __forceinline__ void invert_w1(SrbdLds<1, NM> &S, int t, int ncol, Row<1> &K) {
   const int lane = t & 63;
   int nc = __builtin_amdgcn_readfirstlane(ncol);
   // pivots emitted: 60 when the one-wave class stops at 20 legs (code size)
@@ -552,12 +555,12 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1> &S, int t, int ncol, Row<1>
 }
 
 
-// K0 / K2 table over (row step, column step); column kMaxN is the zero row
-// of padding lanes (cst = kMaxN)
-template <int W>
-__device__ __forceinline__ void fill_k0k2(SrbdLds<W> &S, int N, float Nf, int t) {
-  for (int idx = t; idx < N * (kMaxN + 1); idx += 64 * W) {
-    const int sr = idx / (kMaxN + 1), sc = idx - (kMaxN + 1) * sr;
+// K0 / K2 table over (row step, column step); column NM is the zero row
+// of padding lanes (cst = NM)
+template <int W, int NM>
+__device__ __forceinline__ void fill_k0k2(SrbdLds<W, NM> &S, int N, float Nf, int t) {
+  for (int idx = t; idx < N * (NM + 1); idx += 64 * W) {
+    const int sr = idx / (NM + 1), sc = idx - (NM + 1) * sr;
     float K0 = 0.0f, K2 = 0.0f;
     if (sc < N) k0k2((float)sr, (float)sc, Nf, K0, K2);
     S.k0k2[idx] = (f2v){K0, K2};
@@ -609,6 +612,9 @@ __device__ __forceinline__ void invert_w2(SrbdLds<2> &S, int t, const int (&ncol
 
 // Development-only phase timing (tools/phase_timing.py builds a separate
 // library with -DQLOCO_PHASE_TIMING; the product build never defines it).
+#ifdef QLOCO_TRACE_SIMD
+__device__ unsigned int g_trace[4 << 18];
+#endif
 #ifdef QLOCO_PHASE_TIMING
 __device__ unsigned int g_phase[1 << 20];
 #define QL_PHASE(i)                                                           \
@@ -645,14 +651,21 @@ __device__ unsigned int g_phase[1 << 20];
 #define QLOCO_SMALL_BATCH 6144
 #endif
 constexpr int64_t kSmallBatch = QLOCO_SMALL_BATCH;
+// One-wave kernel for horizons N <= kShortN: LDS tables sized for kShortN,
+// QLOCO_SRBD_SHORT_WPE waves per SIMD (0 disables the instantiation).
+constexpr int kShortN = 10;
+#ifndef QLOCO_SRBD_SHORT_WPE
+#define QLOCO_SRBD_SHORT_WPE 4
+#endif
+constexpr int kShortWpe = QLOCO_SRBD_SHORT_WPE;
 #ifndef QLOCO_SRBD_NUM_VGPR_ATTR  // experiments: force a VGPR budget
 #define QLOCO_SRBD_NUM_VGPR_ATTR
 #endif
 
 // WS: a warm-start mode (1 or 2) may be set.  The cold-start instantiation
 // (the headline path) carries none of the warm / persistent-record code.
-template <int W, bool WS>
-__device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S, const int64_t b) {
+template <int W, bool WS, int NM>
+__device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM> &S, const int64_t b) {
   constexpr int NC = 64 * W, NQ = 16 * W;
   const int t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
@@ -751,7 +764,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
     step = pair >> 2;
     leg = pair & 3;
   }
-  S.cst[t] = valid ? step : kMaxN;
+  S.cst[t] = valid ? step : NM;
   fill_k0k2<W>(S, N, Nf, t);
 
   QL_PHASE(1);
@@ -831,7 +844,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
     S.err[idx] = S.q2[s] * (xf - a.xref[b * 13 * N + 13 * i + s]);
   }
   // rows past the horizon stay zero for good (horizon_rows reads them)
-  for (int idx = 12 * N + t; idx < 12 * kMaxN; idx += NC) S.err[idx] = 0.0f;
+  for (int idx = 12 * N + t; idx < 12 * NM; idx += NC) S.err[idx] = 0.0f;
   bsync<W>();
   row_scans<W>(S, N, false);
   bsync<W>();
@@ -1380,14 +1393,26 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W> &S,
 
 // One instance per workgroup: instance list[blockIdx] (or blockIdx) for
 // list positions below the device-side count (or the batch).
-template <int W, int WPE, bool WS>
+template <int W, int WPE, bool WS, int NM = kMaxN>
 __global__ __launch_bounds__(64 * W)
 __attribute__((amdgpu_waves_per_eu(WPE))) QLOCO_SRBD_NUM_VGPR_ATTR
 void srbd_admm_kernel(const SrbdArgs a) {
-  __shared__ __attribute__((aligned(16))) SrbdLds<W> S;
+  __shared__ __attribute__((aligned(16))) SrbdLds<W, NM> S;
   const int64_t i = blockIdx.x;
   if (i >= (a.count ? (int64_t)*a.count : a.batch)) return;
+#ifdef QLOCO_TRACE_SIMD  // development only (tools/simd_trace.py): placement + wall clock per instance
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   srbd_solve_one<W, WS>(a, S, a.list ? (int64_t)a.list[i] : i);
+#ifdef QLOCO_TRACE_SIMD
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && i < (1 << 18)) {
+    g_trace[4 * i + 0] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID
+    g_trace[4 * i + 1] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // XCC_ID[3:0]
+    g_trace[4 * i + 2] = (unsigned)t0;
+    g_trace[4 * i + 3] = (unsigned)t1;
+  }
+#endif
 }
 
 // Class of every instance by its stance-leg count (<= 21: one wave, <= 42:
@@ -1467,6 +1492,12 @@ extern "C" void qloco_srbd_spec_default(qloco_srbd_spec *s) {
   s->polish = 0;
 }
 
+#ifdef QLOCO_TRACE_SIMD
+extern "C" int qloco_trace_read(unsigned int *host, size_t count) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace), count * sizeof(unsigned int), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 #ifdef QLOCO_PHASE_TIMING
 extern "C" int qloco_phase_read(unsigned int *host, size_t count) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), count * sizeof(unsigned int), 0,
@@ -1618,7 +1649,14 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   const dim3 grid((unsigned)batch);
   auto launch = [&](int cls, hipStream_t s) {
     if (cls == 0) {
-      if (batch <= kSmallBatch) {
+      if (a.N <= kShortN && kShortWpe > 0) {
+        // short horizons: per-step tables sized for N <= 10 (9 KB of LDS) so
+        // 16 one-wave workgroups share a CU -- four waves per SIMD
+        if (ws)
+          hipLaunchKernelGGL((srbd_admm_kernel<1, (kShortWpe > 0 ? kShortWpe : 1), true, kShortN>), grid, dim3(64), 0, s, a);
+        else
+          hipLaunchKernelGGL((srbd_admm_kernel<1, (kShortWpe > 0 ? kShortWpe : 1), false, kShortN>), grid, dim3(64), 0, s, a);
+      } else if (batch <= kSmallBatch) {
         if (ws)
           hipLaunchKernelGGL((srbd_admm_kernel<1, 2, true>), grid, dim3(64), 0, s, a);
         else

@@ -6,6 +6,8 @@ mean / max cycles (s_memtime-style shader clock) at each phase boundary:
 1 inputs+stance, 2 model+gradient, 3 P row, 4 Ruiz, 5 K finalize,
 6 inverse, 7 ADMM loop, 8 outputs.
     python tools/phase_timing.py [variant] [B]
+PHASE_NAME / PHASE_FLAGS (env) build and select a named copy with extra -D
+flags (e.g. PHASE_NAME=row PHASE_FLAGS=-DQLOCO_SRBD_SPLIT=0).
 """
 import ctypes as C
 import os
@@ -15,7 +17,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
-OUT = os.path.join(HERE, "_phase")
+OUT = os.path.join(HERE, "_phase", os.environ.get("PHASE_NAME", "prod"))
+FLAGS = os.environ.get("PHASE_FLAGS", "").split()
 
 
 def build():
@@ -27,7 +30,7 @@ def build():
         obj = os.path.join(OUT, src + ".o")
         if src.endswith(".hip"):
             cmd = ([qb.HIPCC, "--offload-arch=" + qb.ARCH, "-x", "hip"] + qb.COMMON +
-                   qb.EXTRA.get(src, []) + ["-DQLOCO_PHASE_TIMING", "-c", path, "-o", obj])
+                   qb.EXTRA.get(src, []) + ["-DQLOCO_PHASE_TIMING"] + FLAGS + ["-c", path, "-o", obj])
         else:
             cmd = [qb.HIPCC, "-x", "c++"] + qb.COMMON + ["-ffp-contract=off", "-c", path, "-o", obj]
         subprocess.run(cmd, check=True)
@@ -69,7 +72,7 @@ if __name__ == "__main__":
     labels = ["inputs+stance", "model+gradient", "P row", "Ruiz", "K finalize", "inverse",
               "ADMM loop", "outputs"]
     it = out.iters.cpu().numpy()
-    print("variant %s B=%d  mean iters %.1f max %d" % (name, B, it.mean(), it.max()))
+    print("%s variant %s B=%d  mean iters %.1f max %d" % (os.environ.get("PHASE_NAME", "prod"), name, B, it.mean(), it.max()))
     for k, lab in enumerate(labels):
         print("  %-16s mean %9.0f  max %9.0f cycles" % (lab, d[:, k].mean(), d[:, k].max()))
     print("  %-16s mean %9.0f  max %9.0f cycles" % ("TOTAL", ph[:, 8].mean(), ph[:, 8].max()))
