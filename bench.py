@@ -428,7 +428,9 @@ def literal_line(args, srbd, d_x0, d_xr, d_ft, d_ct, stream, dev):
             "executed_frac": round(fe / kt / 1e12 / PEAK_FP32_TFLOPS, 4),
             "note": "the reference's call as written (A1RobotControl.cpp:557-578): all 12N "
                     "forces ADMM variables, swing legs held by fz in [0, 0] equality rows; "
-                    "120 variables per N = 10 instance -> two-wavefront workgroups"}
+                    "%d variables per N = %d instance -> %s" % (
+                        12 * N, N, "two-wavefront workgroups" if 4 * N <= 42
+                        else "512-thread workgroups (srbd_admm_big_kernel)")}
 
 
 def cpu_baseline(N, gait, seconds, threads):

@@ -37,14 +37,34 @@ __constant__ double c_force_CE[5][144];
 // free until the solve starts, and the solver reads only G's lower triangle,
 // copying it in place), so a 4-robot block needs ~18 KB of LDS: 8 blocks per
 // CU, 2 waves per SIMD.
+// Per 4-robot block: each group's g0 and Goldfarb-Idnani work space (the
+// solution is read from gi.x).  The inequality rows are generated
+// (ForceCi), F_leg_guess stays in the owning lane's registers and ce0 is the
+// constant zero vector, so the block stays under 13.3 KB: 12 blocks -- three
+// waves -- per SIMD's share of a CU.
 struct ForceLds {
-  double CI[12 * 24];  // shared by the four groups (constant rows)
-  double ci0[24];
-  double zeros[16];
   struct Grp {
-    double g0[12], x[16], guess[12];
+    double g0[12];
     GiLdsT<12, 24, 12> gi;
   } g[GI_GROUPS];
+};
+
+__constant__ double c_force_zeros[16];
+
+// CI = -qp_H' and ci0 = qp_h of Dynamiccclass (dynmics_compute.cpp:75-98):
+// per leg i, constraint rows 2i / 2i+1 bound fz in [0, fz_max], rows 8+2i,
+// 8+2i+1 and 16+2i, 16+2i+1 the x / y friction pyramid with mu.  CI(v, c) is
+// generated from (v, c) -- the same doubles the matrix holds (0, +-1, mu),
+// so every dot product over it is unchanged.
+struct ForceCi {
+  double mu, fz_max;
+  __device__ __forceinline__ double a(int v, int c, int) const {
+    const int grp = c >> 3, i = (c & 7) >> 1, lo = (c & 1) == 0;
+    if (v == 3 * i + 2) return grp == 0 ? (lo ? 1.0 : -1.0) : mu;
+    if (grp > 0 && v == 3 * i + grp - 1) return lo ? 1.0 : -1.0;
+    return 0.0;
+  }
+  __device__ __forceinline__ double b(int c) const { return (c < 8 && (c & 1)) ? fz_max : 0.0; }
 };
 
 __device__ __forceinline__ double sq(double v) { return v * v; }
@@ -131,38 +151,13 @@ __device__ __forceinline__ void force_distribution(const double *com_des, const 
 }
 
 #ifndef QLOCO_FORCE_WPE  // waves per SIMD the register budget targets
-#define QLOCO_FORCE_WPE 2
+#define QLOCO_FORCE_WPE 3
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_WPE))) void force_qp_kernel(
     const ForceArgs a) {
   __shared__ ForceLds S;
   const int lane = threadIdx.x, grp = lane >> 4, li = lane & 15;
   const int64_t inst = (int64_t)blockIdx.x * GI_GROUPS + grp;
-  // shared constant rows: qp_H / qp_h (dynmics_compute.cpp:75-98), CI = -qp_H'
-  for (int k = lane; k < 12 * 24; k += 64) S.CI[k] = 0.0;
-  if (lane < 16) S.zeros[lane] = 0.0;
-  __syncthreads();
-  if (lane < 4) {
-    const int i = lane;
-    // CI(v, c) = -qpH(c, v), stored CI[c*12 + v]
-    S.CI[(2 * i) * 12 + 3 * i + 2] = 1.0;          // qpH(2i, 3i+2) = -1
-    S.CI[(2 * i + 1) * 12 + 3 * i + 2] = -1.0;     // qpH(2i+1, 3i+2) = 1
-    S.ci0[2 * i] = 0.0;
-    S.ci0[2 * i + 1] = a.fz_max;
-    S.CI[(8 + 2 * i) * 12 + 3 * i] = 1.0;          // qpH(8+2i, 3i) = -1
-    S.CI[(8 + 2 * i) * 12 + 3 * i + 2] = a.mu;     // qpH(8+2i, 3i+2) = -mu
-    S.CI[(8 + 2 * i + 1) * 12 + 3 * i] = -1.0;
-    S.CI[(8 + 2 * i + 1) * 12 + 3 * i + 2] = a.mu;
-    S.ci0[8 + 2 * i] = 0.0;
-    S.ci0[8 + 2 * i + 1] = 0.0;
-    S.CI[(16 + 2 * i) * 12 + 3 * i + 1] = 1.0;
-    S.CI[(16 + 2 * i) * 12 + 3 * i + 2] = a.mu;
-    S.CI[(16 + 2 * i + 1) * 12 + 3 * i + 1] = -1.0;
-    S.CI[(16 + 2 * i + 1) * 12 + 3 * i + 2] = a.mu;
-    S.ci0[16 + 2 * i] = 0.0;
-    S.ci0[16 + 2 * i + 1] = 0.0;
-  }
-  __syncthreads();
   if (inst >= a.batch) return;
   ForceLds::Grp &P = S.g[grp];
   double *const PA = P.gi.J;  // A, 6x12 col-major (dead before J is formed)
@@ -176,12 +171,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_
                      Fref);
   // this lane's entry by a static select chain: indexing Fref by li would put
   // the array in scratch (a per-lane spill of 96 B, written back to HBM)
-  {
-    double mine = Fref[0];
+  double guess = Fref[0];  // F_leg_guess entry li (only lane li reads it)
 #pragma unroll
-    for (int k = 1; k < 12; ++k) mine = (li == k) ? Fref[k] : mine;
-    if (li < 12) P.guess[li] = mine;
-  }
+  for (int k = 1; k < 12; ++k) guess = (li == k) ? Fref[k] : guess;
   // ---- force_opt: A (6x12, col-major) with the skew_hat quirk (:274-298)
   if (li < 12) {
     for (int k = 0; k < 6; ++k) PA[li * 6 + k] = 0.0;
@@ -217,7 +209,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_
     double atf = 0.0;
     const double *FT = a.FT_total_des + inst * 6;
     for (int k = 0; k < 6; ++k) atf += PA[r * 6 + k] * FT[k];
-    P.g0[r] = -2.0 * (a.alpha * atf + a.beta * P.guess[r] + a.gamma * a.grf_opt[inst * 12 + r]);
+    P.g0[r] = -2.0 * (a.alpha * atf + a.beta * guess + a.gamma * a.grf_opt[inst * 12 + r]);
   }
   GI_SYNC();
   // swing-leg equality pattern AA (:310-350)
@@ -230,10 +222,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_
   double f;
   int st, it;
 #ifndef QLOCO_ABLATE_FORCE_GI
-  gi_solve_group(P.gi, li, 12, 12, 24, PG, 12, P.g0, c_force_CE[pat], S.zeros, S.CI, S.ci0, P.x,
+  gi_solve_group(P.gi, li, 12, 12, 24, PG, 12, P.g0, c_force_CE[pat], c_force_zeros,
+                 ForceCi{a.mu, a.fz_max}, P.gi.x,
                  f, st, it);
 #else  // timing experiments only (tools/variant_lib.py): everything but the solve
-  if (li < 12) P.x[li] = P.g0[li] * 1e-9;
+  if (li < 12) P.gi.x[li] = P.g0[li] * 1e-9;
   f = 0.0;
   st = 0;
   it = pat;
@@ -241,11 +234,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_
   GI_SYNC();
   // QPBaseClass::solveQP: success iff no NaN (go1_rt_control QPBaseClass.cpp:116-142); Solve / fallback
   bool ok = true;
-  for (int k = 0; k < 12; ++k) ok = ok && !isnan(P.x[k]);
+  for (int k = 0; k < 12; ++k) ok = ok && !isnan(P.gi.x[k]);
   if (li < 12) {
-    a.grf_opt[inst * 12 + li] = ok ? P.x[li] : P.guess[li];
-    a.F_leg_guess[inst * 12 + li] = P.guess[li];
-    a.F_leg_ref[inst * 12 + li] = P.guess[li];  // = Fref (F_leg_guess := F_leg_ref, :251-260)
+    a.grf_opt[inst * 12 + li] = ok ? P.gi.x[li] : guess;
+    a.F_leg_guess[inst * 12 + li] = guess;
+    a.F_leg_ref[inst * 12 + li] = guess;  // = Fref (F_leg_guess := F_leg_ref, :251-260)
   }
   if (li == 0) {
     if (a.qp_solution) a.qp_solution[inst] = ok ? 1 : 0;
