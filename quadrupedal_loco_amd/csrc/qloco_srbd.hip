@@ -412,7 +412,7 @@ __device__ __forceinline__ PCoef p_coef(const SrbdLds<W, NM> &S, f4v lo, f4v hi,
 // come in leg triples (lanes 3l..3l+2 of a wave, lane 63 padding), so the
 // column component is static and K0 / K2 -- functions of the row and column
 // steps only -- are one LDS table read per triple.
-template <int W, int NM>
+template <int W, int C2, int NM>
 __device__ __forceinline__ void gen_p_row(const SrbdLds<W, NM> &S, const PCoef &pc, int t, bool valid,
                                           int step, int comp, float r2v, Row<W> &K) {
   // opaque copies: keep LICM from hoisting per-column selects out of the ADMM loop
@@ -427,8 +427,10 @@ __device__ __forceinline__ void gen_p_row(const SrbdLds<W, NM> &S, const PCoef &
                "+v"(le1), "+v"(le2));
 #pragma unroll
   for (int h = 0; h < W; ++h) {
+    // the second half of a two-wave row stops at its bucket's 4 C2 columns
+    constexpr int kNarrow = W == 2 && C2 < 16;
 #pragma unroll
-    for (int l = 0; l < kLegsPerWave; ++l) {
+    for (int l = 0; l < ((h == 1 && kNarrow) ? 4 * C2 / 3 : kLegsPerWave); ++l) {
       __builtin_amdgcn_sched_barrier(0);  // bound live ranges: one triple at a time
       const int c0 = 64 * h + 3 * l;
       const f2v kk = S.k0k2[kb + S.cst[c0]];
@@ -445,37 +447,43 @@ __device__ __forceinline__ void gen_p_row(const SrbdLds<W, NM> &S, const PCoef &
         KE(K, c) = pv;
       }
     }
-    KE(K, 64 * h + 63) = (64 * h + 63 == tt) ? dadd : 0.0f;  // padding column
+    if (!(h == 1 && kNarrow))
+      KE(K, 64 * h + 63) = (64 * h + 63 == tt) ? dadd : 0.0f;  // padding column
   }
 }
 
 // W = 2: the second half of a row (columns 64..) holds ncol[1] valid
-// columns; its DPP forms run 9 (<= 36 columns), 15 (<= 60) or 16 chunks.
-// The padding columns beyond are identity (zero on valid rows), so the
-// shorter forms are exact.
-__device__ __forceinline__ int half2_chunks(int ncol1) {
-  return ncol1 <= 36 ? 9 : (ncol1 <= 60 ? 15 : 16);
-}
-#define QL_HALF2(C2, NAME36, NAME60, NAME64, ...) \
-  do {                                           \
-    if ((C2) == 9) {                             \
-      NAME36(__VA_ARGS__);                       \
-    } else if ((C2) == 15) {                     \
-      NAME60(__VA_ARGS__);                       \
-    } else {                                     \
-      NAME64(__VA_ARGS__);                       \
-    }                                            \
+// columns.  Each two-wave kernel is instantiated for one bucket C2 of them
+// (3, 6, 9 or 15 DPP chunks: <= 12, 24, 36 or 60 columns, i.e. 21-25, 26-29,
+// 30-33 or 34-41 stance legs; 42 legs go to the wide kernel); the padding
+// columns beyond are identity (zero on valid rows), so the shorter forms
+// are exact, and the registers of the columns a bucket never touches are
+// not allocated at all.
+constexpr int w2_bucket_legs(int c2) { return kLegsPerWave + (c2 < 16 ? 4 * c2 / 3 : kLegsPerWave); }
+#define QL_HALF2(C2, NAME12, NAME24, NAME36, NAME60, NAME64, ...) \
+  do {                                                           \
+    if constexpr ((C2) == 3) {                                   \
+      NAME12(__VA_ARGS__);                                       \
+    } else if constexpr ((C2) == 6) {                            \
+      NAME24(__VA_ARGS__);                                       \
+    } else if constexpr ((C2) == 9) {                            \
+      NAME36(__VA_ARGS__);                                       \
+    } else if constexpr ((C2) == 15) {                           \
+      NAME60(__VA_ARGS__);                                       \
+    } else {                                                     \
+      NAME64(__VA_ARGS__);                                       \
+    }                                                            \
   } while (0)
 
 // K_rc <- rs * D_c * P_rc + [sigma I + A' diag(rho) A]_rc, the leg block
 // touching only the lane's own leg columns (static column -> leg map; D_c
 // fanned out from one LDS chunk per lane by DPP).  Returns the diagonal
 // (pivot tracking of the W = 2 inverse).
-template <int W, int NM>
+template <int W, int C2, int NM>
 __device__ __forceinline__ float finalize_row(const SrbdLds<W, NM> &S, int t, int cbase, float rs,
                                               float add0, float add1, float add2, bool c60,
-                                              int c2, Row<W> &K) {
-  constexpr int NC = 64 * W;
+                                              Row<W> &K) {
+  constexpr int NC = W == 1 ? 64 : 64 + 4 * C2;
   const int lane = t & 63;
   const f4v d0 = reinterpret_cast<const f4v *>(S.Dc)[lane & 15];
   if (W == 1 && c60) {  // padding columns 60..63 have D = 1
@@ -485,7 +493,7 @@ __device__ __forceinline__ float finalize_row(const SrbdLds<W, NM> &S, int t, in
   }
   if constexpr (W == 2) {
     const f4v d1 = reinterpret_cast<const f4v *>(S.Dc)[16 + (lane & 15)];
-    QL_HALF2(c2, QL_DPP_MUL36, QL_DPP_MUL60, QL_DPP_MUL64, K.k, 64, d1);
+    QL_HALF2(C2, QL_DPP_MUL12, QL_DPP_MUL24, QL_DPP_MUL36, QL_DPP_MUL60, QL_DPP_MUL64, K.k, 64, d1);
   }
   int cb = cbase, tt = t;
   asm volatile("" : "+v"(cb), "+v"(tt));
@@ -571,12 +579,12 @@ __device__ __forceinline__ void fill_k0k2(SrbdLds<W, NM> &S, int N, float Nf, in
 // Two-wave form: the same transposed write, one pivot half per wave (the
 // pivot column register is static inside each half), one s_barrier per
 // pivot, the pivot value through LDS.
-template <int H>
-__device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, int c2, Row<2> &K) {
+template <int H, int C2>
+__device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, Row<2> &K) {
   const int lane = t & 63;
   int nc = __builtin_amdgcn_readfirstlane(nw);
 #pragma unroll
-  for (int kk = 0; kk < 64; ++kk) {
+  for (int kk = 0; kk < (H == 1 ? 4 * C2 : 64); ++kk) {
     asm volatile("" : "+s"(nc));
     if (kk >= nc) continue;  // block-uniform
     const int k = 64 * H + kk;
@@ -593,20 +601,19 @@ __device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, int
     const float pinv = __builtin_amdgcn_rcpf(p);
     const float ng = -((tt == k) ? (1.0f - pinv) : v * pinv);
     QL_DPP_GJ64(K.k, 0, r0, ng);
-    (void)c2;  // one form: per-bucket forms triple the (instruction-cache bound) code
-    QL_DPP_GJ64(K.k, 64, r1, ng);
+    QL_HALF2(C2, QL_DPP_GJ12, QL_DPP_GJ24, QL_DPP_GJ36, QL_DPP_GJ60, QL_DPP_GJ64, K.k, 64, r1, ng);
     if (p > kGjExactPivot) K.k[k] = (tt == k) ? pinv : ng;  // column k exactly (invert_w1)
   }
 }
 
-__device__ __forceinline__ void invert_w2(SrbdLds<2> &S, int t, const int (&ncol)[2], int c2,
-                                          Row<2> &K) {
-  invert_w2_half<0>(S, t, ncol[0], c2, K);
+template <int C2>
+__device__ __forceinline__ void invert_w2(SrbdLds<2> &S, int t, const int (&ncol)[2], Row<2> &K) {
+  invert_w2_half<0, C2>(S, t, ncol[0], K);
   // the buffer parity restarts with the second half (its first pivot may
   // reuse the buffer of the first half's last one): all reads of that
   // buffer must be done before it is rewritten
   __syncthreads();
-  invert_w2_half<1>(S, t, ncol[1], c2, K);
+  invert_w2_half<1, C2>(S, t, ncol[1], K);
   __syncthreads();
 }
 
@@ -664,9 +671,10 @@ constexpr int kShortWpe = QLOCO_SRBD_SHORT_WPE;
 
 // WS: a warm-start mode (1 or 2) may be set.  The cold-start instantiation
 // (the headline path) carries none of the warm / persistent-record code.
-template <int W, bool WS, int NM>
+template <int W, bool WS, int NM, int C2 = 16>
 __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM> &S, const int64_t b) {
   constexpr int NC = 64 * W, NQ = 16 * W;
+  constexpr int NK = W == 1 ? 64 : 64 + 4 * C2;  // register columns of K the bucket touches
   const int t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
 #ifdef QLOCO_PHASE_TIMING
@@ -717,7 +725,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
   const int nlegs = uni(S.nlegs);
   const int n = 3 * nlegs;
   if (nlegs < a.leg_lo || nlegs > a.leg_hi) return;  // the other launch's instance
-  if (nlegs > (W == 1 ? kW1Legs : kLegsPerWave * W)) {  // uniform: the caller's max_stance_legs was too small
+  if (nlegs > (W == 1 ? kW1Legs : w2_bucket_legs(C2))) {  // uniform: the caller's max_stance_legs was too small
     if (t < 12) a.u0[b * 12 + t] = NAN;
     if (a.u)
       for (int k = t; k < 12 * N; k += NC) a.u[b * 12 * N + k] = NAN;
@@ -754,7 +762,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
   }
   // every valid column below 60: the 60-column DPP forms (uniform)
   const bool c60 = W == 1 && (kW1Legs <= 20 || __builtin_amdgcn_readfirstlane(ncol[0]) <= 60);
-  const int c2 = W == 2 ? half2_chunks(__builtin_amdgcn_readfirstlane(ncol[W - 1])) : 16;
   const int lslot = lane / 3;
   const int comp = lane - 3 * lslot;
   const bool valid = (lane < 63) && (kLegsPerWave * wave + lslot < nlegs);
@@ -970,7 +977,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
     {  // closed-form P row, regenerated for every factorisation
       const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
       const PCoef pc = p_coef<W>(S, blo, bhi, comp, valid, dtm, dt2m);
-      gen_p_row<W>(S, pc, t, valid, (int)bhi.z, comp, S.aux[0][t], K);
+      gen_p_row<W, C2>(S, pc, t, valid, (int)bhi.z, comp, S.aux[0][t], K);
     }
     if (first) {
       QL_PHASE(3);
@@ -979,7 +986,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       // the DPP-fanned D chunk
       float cnP = 0.0f;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) cnP = fmaxf(cnP, fabsf(KE(K, c)));
+      for (int c = 0; c < NK; ++c) cnP = fmaxf(cnP, fabsf(KE(K, c)));
       const float inv_n = 1.0f / (float)(n > 0 ? n : 1);
       for (int it = 0; it < a.scaling; ++it) {
         QL_PSTAMP(_r0);
@@ -1018,8 +1025,8 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
           }
           if constexpr (W == 2) {
             const f4v d1 = S.bc[buf][16 + (lane & 15)];
-            QL_HALF2(c2, QL_DPP_ABSMAX36, QL_DPP_ABSMAX60, QL_DPP_ABSMAX64, m0, m1, m2, m3, t0, t1,
-                     t2, t3, d1, K.k, 64);
+            QL_HALF2(C2, QL_DPP_ABSMAX12, QL_DPP_ABSMAX24, QL_DPP_ABSMAX36, QL_DPP_ABSMAX60, QL_DPP_ABSMAX64, m0, m1,
+                     m2, m3, t0, t1, t2, t3, d1, K.k, 64);
           }
         }
         // row norm of D P D after this pass (without the running cost scale)
@@ -1065,7 +1072,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
     {
       float add0, add1, add2;
       leg_block(add0, add1, add2);
-      const float dg = finalize_row<W>(S, t, t - comp, cs * S.Dc[t], add0, add1, add2, c60, c2, K);
+      const float dg = finalize_row<W, C2>(S, t, t - comp, cs * S.Dc[t], add0, add1, add2, c60, K);
 #ifdef QLOCO_DEBUG_INST
       if (b == QLOCO_DEBUG_INST) {
         float kd = 0.0f;
@@ -1093,7 +1100,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         }
       } else {
         (void)dg;
-        invert_w2(S, t, ncol, c2, K);
+        invert_w2<C2>(S, t, ncol, K);
       }
       if (first) QL_PHASE(6);
 #ifdef QLOCO_DEBUG_INST  // development only (tools/variant_lib.py): inverse health of one instance
@@ -1215,7 +1222,11 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
             QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r0, K.k, 0);
             if constexpr (W == 2) {
               const f4v r1 = S.bc[buf][16 + (lane & 15)];
-              if constexpr (CH == 9) {
+              if constexpr (CH == 3) {
+                QL_DPP_MATVEC12_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
+              } else if constexpr (CH == 6) {
+                QL_DPP_MATVEC24_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
+              } else if constexpr (CH == 9) {
                 QL_DPP_MATVEC36_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
               } else if constexpr (CH == 15) {
                 QL_DPP_MATVEC60_ACC(acc0, acc1, acc2, acc3, r1, K.k, 64);
@@ -1258,13 +1269,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
           run_block(std::false_type{}, std::integral_constant<int, 16>{});
         }
       } else {
-        if (c2 == 9) {
-          run_block(std::false_type{}, std::integral_constant<int, 9>{});
-        } else if (c2 == 15) {
-          run_block(std::false_type{}, std::integral_constant<int, 15>{});
-        } else {
-          run_block(std::false_type{}, std::integral_constant<int, 16>{});
-        }
+        run_block(std::false_type{}, std::integral_constant<int, C2>{});
       }
       }
       // OSQP: termination check every check_termination iterations, rho
@@ -1393,7 +1398,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
 
 // One instance per workgroup: instance list[blockIdx] (or blockIdx) for
 // list positions below the device-side count (or the batch).
-template <int W, int WPE, bool WS, int NM = kMaxN>
+template <int W, int WPE, bool WS, int NM = kMaxN, int C2 = 16>
 __global__ __launch_bounds__(64 * W)
 __attribute__((amdgpu_waves_per_eu(WPE))) QLOCO_SRBD_NUM_VGPR_ATTR
 void srbd_admm_kernel(const SrbdArgs a) {
@@ -1403,7 +1408,7 @@ void srbd_admm_kernel(const SrbdArgs a) {
 #ifdef QLOCO_TRACE_SIMD  // development only (tools/simd_trace.py): placement + wall clock per instance
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  srbd_solve_one<W, WS>(a, S, a.list ? (int64_t)a.list[i] : i);
+  srbd_solve_one<W, WS, NM, C2>(a, S, a.list ? (int64_t)a.list[i] : i);
 #ifdef QLOCO_TRACE_SIMD
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0 && i < (1 << 18)) {
@@ -1415,10 +1420,23 @@ void srbd_admm_kernel(const SrbdArgs a) {
 #endif
 }
 
-// Class of every instance by its stance-leg count (<= 21: one wave, <= 42:
-// two waves, else the wide kernel; capped at the top class the launch
-// admits), appended to that class's list: one ballot per class and wave,
-// one atomic per wave and class (list order within a wave is instance order).
+// Kernel classes by stance-leg count: 0 one wave (<= kW1Legs), 1..4 two
+// waves in the column buckets C2 = 3 / 6 / 9 / 15 (<= 25 / 29 / 33 / 41
+// legs), 5 the wide kernel.  Warm-started launches use bucket 4 for every
+// two-wave instance (one warm two-wave instantiation).
+constexpr int kSrbdClasses = 6;
+__host__ __device__ constexpr int srbd_class_of(int legs, bool ws) {
+  return legs <= kW1Legs ? 0
+         : legs <= w2_bucket_legs(15)
+             ? (ws ? 4
+                   : (legs <= w2_bucket_legs(3) ? 1
+                      : legs <= w2_bucket_legs(6) ? 2 : legs <= w2_bucket_legs(9) ? 3 : 4))
+             : 5;
+}
+
+// Class of every instance (capped at the top class the launch admits),
+// appended to that class's list: one ballot per class and wave, one atomic
+// per wave and class (list order within a wave is instance order).
 __global__ __launch_bounds__(256) void srbd_classify_kernel(const SrbdArgs a, int top, int *lists,
                                                             int64_t cap, int *counts) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1435,7 +1453,7 @@ __global__ __launch_bounds__(256) void srbd_classify_kernel(const SrbdArgs a, in
       for (int k = 0; k < 4; ++k) legs += a.contacts[b * 4 + k] != 0;
       legs *= N;
     }
-    cls = legs <= kW1Legs ? 0 : (legs <= 2 * kLegsPerWave ? 1 : 2);
+    cls = srbd_class_of(legs, a.warm_start != 0);
     cls = cls > top ? top : cls;
   }
   const int lane = threadIdx.x & 63;
@@ -1544,7 +1562,7 @@ static int srbd_scratch(int64_t batch, hipStream_t st, SrbdScratch **out) {
     }
   }
   if (fresh) {
-    if (hipMalloc(&s.counts, 4 * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
+    if (hipMalloc(&s.counts, 8 * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
     for (int k = 0; k < 2; ++k) {
       if (hipStreamCreateWithFlags(&s.side[k], hipStreamNonBlocking) != hipSuccess) return QLOCO_ERR_DEVICE;
       if (hipEventCreateWithFlags(&s.join[k], hipEventDisableTiming) != hipSuccess) return QLOCO_ERR_DEVICE;
@@ -1554,7 +1572,7 @@ static int srbd_scratch(int64_t batch, hipStream_t st, SrbdScratch **out) {
   if (batch > s.cap) {
     const int64_t cap = batch < 4096 ? 4096 : batch;
     int *lists = nullptr;
-    if (hipMalloc(&lists, 3 * cap * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
+    if (hipMalloc(&lists, kSrbdClasses * cap * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
     if (s.lists) g_srbd_retired.push_back(s.lists);
     s.lists = lists;
     s.cap = cap;
@@ -1667,11 +1685,19 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
         else
           hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, false>), grid, dim3(64), 0, s, a);
       }
-    } else if (cls == 1) {
-      if (ws)
-        hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, true>), grid, dim3(128), 0, s, a);
+    } else if (cls <= 4) {  // two-wave column buckets C2 = 3 / 6 / 9 / 15
+      constexpr int WP = QLOCO_SRBD_WAVES_PER_EU_W2;
+      if (ws)  // srbd_class_of routes every warm two-wave instance to bucket 4
+        hipLaunchKernelGGL((srbd_admm_kernel<2, WP, true, kMaxN, 15>), grid, dim3(128), 0, s, a);
+      // the narrow buckets fit 168 VGPRs: three waves per SIMD
+      else if (cls == 1)
+        hipLaunchKernelGGL((srbd_admm_kernel<2, 3, false, kMaxN, 3>), grid, dim3(128), 0, s, a);
+      else if (cls == 2)
+        hipLaunchKernelGGL((srbd_admm_kernel<2, 3, false, kMaxN, 6>), grid, dim3(128), 0, s, a);
+      else if (cls == 3)
+        hipLaunchKernelGGL((srbd_admm_kernel<2, WP, false, kMaxN, 9>), grid, dim3(128), 0, s, a);
       else
-        hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_WAVES_PER_EU_W2, false>), grid, dim3(128), 0, s, a);
+        hipLaunchKernelGGL((srbd_admm_kernel<2, WP, false, kMaxN, 15>), grid, dim3(128), 0, s, a);
     } else {
       if (ws)
         hipLaunchKernelGGL((srbd_admm_big_kernel<true>), grid, dim3(kBigThreads), 0, s, a);
@@ -1679,7 +1705,7 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
         hipLaunchKernelGGL((srbd_admm_big_kernel<false>), grid, dim3(kBigThreads), 0, s, a);
     }
   };
-  const int top = legs <= kW1Legs ? 0 : (legs <= 2 * kLegsPerWave ? 1 : 2);
+  const int top = srbd_class_of(legs, ws);
   if (top == 0 || a.literal) {
     // one class: every instance of the literal QP has 4N leg triples, so no
     // classification and no empty class launches
@@ -1689,27 +1715,36 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
     SrbdScratch *sc = nullptr;
     const int rc = srbd_scratch(batch, st, &sc);
     if (rc != QLOCO_OK) return rc;
-    QLOCO_HIP_CHECK(hipMemsetAsync(sc->counts, 0, 4 * sizeof(int), st), "class counters");
+    QLOCO_HIP_CHECK(hipMemsetAsync(sc->counts, 0, 8 * sizeof(int), st), "class counters");
     hipLaunchKernelGGL(srbd_classify_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st,
                        a, top, sc->lists, sc->cap, sc->counts);
     QLOCO_HIP_CHECK(hipGetLastError(), "srbd_classify_kernel launch");
     const bool fork = srbd_fork_enabled();
     if (fork) QLOCO_HIP_CHECK(hipEventRecord(sc->fork, st), "fork event");
+    // class 0 on the caller's stream, the two-wave buckets in order on side
+    // stream 0, the wide kernel on side stream 1
+    bool waited[2] = {false, false};
+    int last[2] = {-1, -1};
+    for (int c = 0; c <= top; ++c)
+      if (c > 0 && !(ws && c >= 1 && c <= 3)) last[c == 5 ? 1 : 0] = c;
     for (int c = 0; c <= top; ++c) {
+      if (ws && c >= 1 && c <= 3) continue;  // empty by construction (srbd_class_of)
       a.list = sc->lists + (int64_t)c * sc->cap;
       a.count = sc->counts + c;
       a.leg_lo = 0;
       a.leg_hi = 1 << 30;
+      const int sd = c == 5 ? 1 : 0;
       hipStream_t s = st;
       if (fork && c > 0) {
-        s = sc->side[c - 1];
-        QLOCO_HIP_CHECK(hipStreamWaitEvent(s, sc->fork, 0), "fork wait");
+        s = sc->side[sd];
+        if (!waited[sd]) QLOCO_HIP_CHECK(hipStreamWaitEvent(s, sc->fork, 0), "fork wait");
+        waited[sd] = true;
       }
       launch(c, s);
       QLOCO_HIP_CHECK(hipGetLastError(), "srbd class kernel launch");
-      if (fork && c > 0) {
-        QLOCO_HIP_CHECK(hipEventRecord(sc->join[c - 1], s), "join event");
-        QLOCO_HIP_CHECK(hipStreamWaitEvent(st, sc->join[c - 1], 0), "join wait");
+      if (fork && c > 0 && c == last[sd]) {
+        QLOCO_HIP_CHECK(hipEventRecord(sc->join[sd], s), "join event");
+        QLOCO_HIP_CHECK(hipStreamWaitEvent(st, sc->join[sd], 0), "join wait");
       }
     }
   }

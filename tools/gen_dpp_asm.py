@@ -120,5 +120,9 @@ if __name__ == "__main__":
                 matvec(True, 15) + "\n" + matvec(True, 9) + "\n" + gj(9) + "\n" + mul(9) + "\n" +
                 absmax(9) + "\n" +
                 # four-chain 60-column form (W = 1, QLOCO_MATVEC4)
-                matvec(False, 15))
+                matvec(False, 15) + "\n" +
+                # W = 2 second-half forms for the narrow buckets (<= 12 / <= 24
+                # columns: 22-25 / 26-29 stance legs, the mixed schedules)
+                matvec(True, 3) + "\n" + matvec(True, 6) + "\n" + gj(3) + "\n" + gj(6) + "\n" +
+                mul(3) + "\n" + mul(6) + "\n" + absmax(3) + "\n" + absmax(6))
     print(OUT)
