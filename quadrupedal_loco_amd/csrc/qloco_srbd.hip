@@ -427,10 +427,12 @@ __device__ __forceinline__ void gen_p_row(const SrbdLds<W, NM> &S, const PCoef &
                "+v"(le1), "+v"(le2));
 #pragma unroll
   for (int h = 0; h < W; ++h) {
-    // the second half of a two-wave row stops at its bucket's 4 C2 columns
-    constexpr int kNarrow = W == 2 && C2 < 16;
+    // the second half of a two-wave row stops at its bucket's 4 C2 columns,
+    // a one-wave row at kW1Legs legs (60 columns: 60..63 never allocated)
+    constexpr bool kNarrow = W == 2 && C2 < 16;
+    constexpr bool kW1Narrow = W == 1 && kW1Legs <= 20;
 #pragma unroll
-    for (int l = 0; l < ((h == 1 && kNarrow) ? 4 * C2 / 3 : kLegsPerWave); ++l) {
+    for (int l = 0; l < ((h == 1 && kNarrow) ? 4 * C2 / 3 : (kW1Narrow ? kW1Legs : kLegsPerWave)); ++l) {
       __builtin_amdgcn_sched_barrier(0);  // bound live ranges: one triple at a time
       const int c0 = 64 * h + 3 * l;
       const f2v kk = S.k0k2[kb + S.cst[c0]];
@@ -447,7 +449,7 @@ __device__ __forceinline__ void gen_p_row(const SrbdLds<W, NM> &S, const PCoef &
         KE(K, c) = pv;
       }
     }
-    if (!(h == 1 && kNarrow))
+    if (!(h == 1 && kNarrow) && !kW1Narrow)
       KE(K, 64 * h + 63) = (64 * h + 63 == tt) ? dadd : 0.0f;  // padding column
   }
 }
@@ -483,7 +485,7 @@ template <int W, int C2, int NM>
 __device__ __forceinline__ float finalize_row(const SrbdLds<W, NM> &S, int t, int cbase, float rs,
                                               float add0, float add1, float add2, bool c60,
                                               Row<W> &K) {
-  constexpr int NC = W == 1 ? 64 : 64 + 4 * C2;
+  constexpr int NC = W == 1 ? (kW1Legs <= 20 ? 60 : 64) : 64 + 4 * C2;
   const int lane = t & 63;
   const f4v d0 = reinterpret_cast<const f4v *>(S.Dc)[lane & 15];
   if (W == 1 && c60) {  // padding columns 60..63 have D = 1
@@ -674,7 +676,7 @@ constexpr int kShortWpe = QLOCO_SRBD_SHORT_WPE;
 template <int W, bool WS, int NM, int C2 = 16>
 __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM> &S, const int64_t b) {
   constexpr int NC = 64 * W, NQ = 16 * W;
-  constexpr int NK = W == 1 ? 64 : 64 + 4 * C2;  // register columns of K the bucket touches
+  constexpr int NK = W == 1 ? (kW1Legs <= 20 ? 60 : 64) : 64 + 4 * C2;  // register columns of K in use
   const int t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
 #ifdef QLOCO_PHASE_TIMING
