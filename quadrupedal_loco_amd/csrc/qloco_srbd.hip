@@ -644,6 +644,9 @@ __device__ unsigned int g_phase[1 << 20];
 #define QL_PACC(i, v0) ((void)0)
 #endif
 
+#ifndef QLOCO_SRBD_W2_C9_WPE  // occupancy of the C2 = 9 two-wave bucket (30-33 legs, N = 16 trot)
+#define QLOCO_SRBD_W2_C9_WPE 3
+#endif
 #ifndef QLOCO_SRBD_WAVES_PER_EU_W2  // two-wave kernel occupancy
 #define QLOCO_SRBD_WAVES_PER_EU_W2 2
 #endif
@@ -1424,16 +1427,18 @@ void srbd_admm_kernel(const SrbdArgs a) {
 
 // Kernel classes by stance-leg count: 0 one wave (<= kW1Legs), 1..4 two
 // waves in the column buckets C2 = 3 / 6 / 9 / 15 (<= 25 / 29 / 33 / 41
-// legs), 5 the wide kernel.  Warm-started launches use bucket 4 for every
-// two-wave instance (one warm two-wave instantiation).
-constexpr int kSrbdClasses = 6;
+// legs), 5..7 the wide kernel at half widths 96 / 112 / 120 (<= 64 / 74 /
+// 80 legs; qloco_srbd_big.inc).  Warm-started launches use the widest
+// bucket of each family (one warm instantiation per family).
+constexpr int kSrbdClasses = 8;
+constexpr int kBigLegs64 = 64, kBigLegs74 = 74;  // = big_bucket_legs(96 / 112)
 __host__ __device__ constexpr int srbd_class_of(int legs, bool ws) {
   return legs <= kW1Legs ? 0
          : legs <= w2_bucket_legs(15)
              ? (ws ? 4
                    : (legs <= w2_bucket_legs(3) ? 1
                       : legs <= w2_bucket_legs(6) ? 2 : legs <= w2_bucket_legs(9) ? 3 : 4))
-             : 5;
+             : (ws ? 7 : (legs <= kBigLegs64 ? 5 : legs <= kBigLegs74 ? 6 : 7));
 }
 
 // Class of every instance (capped at the top class the launch admits),
@@ -1697,14 +1702,19 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
       else if (cls == 2)
         hipLaunchKernelGGL((srbd_admm_kernel<2, 3, false, kMaxN, 6>), grid, dim3(128), 0, s, a);
       else if (cls == 3)
-        hipLaunchKernelGGL((srbd_admm_kernel<2, WP, false, kMaxN, 9>), grid, dim3(128), 0, s, a);
+        hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_W2_C9_WPE, false, kMaxN, 9>), grid, dim3(128), 0, s, a);
       else
         hipLaunchKernelGGL((srbd_admm_kernel<2, WP, false, kMaxN, 15>), grid, dim3(128), 0, s, a);
-    } else {
-      if (ws)
-        hipLaunchKernelGGL((srbd_admm_big_kernel<true>), grid, dim3(kBigThreads), 0, s, a);
+    } else {  // wide kernel half widths HC = 96 / 112 / 120
+      if (ws)  // srbd_class_of routes every warm wide instance to class 7: one
+               // warm instantiation at the full 128-column halves
+        hipLaunchKernelGGL((srbd_admm_big_kernel<true, 128>), grid, dim3(kBigThreads), 0, s, a);
+      else if (cls == 5)
+        hipLaunchKernelGGL((srbd_admm_big_kernel<false, 96>), grid, dim3(kBigThreads), 0, s, a);
+      else if (cls == 6)
+        hipLaunchKernelGGL((srbd_admm_big_kernel<false, 112>), grid, dim3(kBigThreads), 0, s, a);
       else
-        hipLaunchKernelGGL((srbd_admm_big_kernel<false>), grid, dim3(kBigThreads), 0, s, a);
+        hipLaunchKernelGGL((srbd_admm_big_kernel<false, 120>), grid, dim3(kBigThreads), 0, s, a);
     }
   };
   const int top = srbd_class_of(legs, ws);
@@ -1724,18 +1734,21 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
     const bool fork = srbd_fork_enabled();
     if (fork) QLOCO_HIP_CHECK(hipEventRecord(sc->fork, st), "fork event");
     // class 0 on the caller's stream, the two-wave buckets in order on side
-    // stream 0, the wide kernel on side stream 1
+    // stream 0, the wide buckets in order on side stream 1
     bool waited[2] = {false, false};
     int last[2] = {-1, -1};
+    auto skip = [&](int c) {  // empty by construction (srbd_class_of)
+      return ws && ((c >= 1 && c <= 3) || c == 5 || c == 6);
+    };
     for (int c = 0; c <= top; ++c)
-      if (c > 0 && !(ws && c >= 1 && c <= 3)) last[c == 5 ? 1 : 0] = c;
+      if (c > 0 && !skip(c)) last[c >= 5 ? 1 : 0] = c;
     for (int c = 0; c <= top; ++c) {
-      if (ws && c >= 1 && c <= 3) continue;  // empty by construction (srbd_class_of)
+      if (skip(c)) continue;
       a.list = sc->lists + (int64_t)c * sc->cap;
       a.count = sc->counts + c;
       a.leg_lo = 0;
       a.leg_hi = 1 << 30;
-      const int sd = c == 5 ? 1 : 0;
+      const int sd = c >= 5 ? 1 : 0;
       hipStream_t s = st;
       if (fork && c > 0) {
         s = sc->side[sd];
