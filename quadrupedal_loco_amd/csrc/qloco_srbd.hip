@@ -647,6 +647,9 @@ __device__ unsigned int g_phase[1 << 20];
 #ifndef QLOCO_SRBD_W2_C9_WPE  // occupancy of the C2 = 9 two-wave bucket (30-33 legs, N = 16 trot)
 #define QLOCO_SRBD_W2_C9_WPE 3
 #endif
+#ifndef QLOCO_SRBD_W2_C15_WPE  // occupancy of the C2 = 15 two-wave bucket (34-41 legs, N = 20 pace)
+#define QLOCO_SRBD_W2_C15_WPE 3
+#endif
 #ifndef QLOCO_SRBD_WAVES_PER_EU_W2  // two-wave kernel occupancy
 #define QLOCO_SRBD_WAVES_PER_EU_W2 2
 #endif
@@ -1704,7 +1707,7 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
       else if (cls == 3)
         hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_W2_C9_WPE, false, kMaxN, 9>), grid, dim3(128), 0, s, a);
       else
-        hipLaunchKernelGGL((srbd_admm_kernel<2, WP, false, kMaxN, 15>), grid, dim3(128), 0, s, a);
+        hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_W2_C15_WPE, false, kMaxN, 15>), grid, dim3(128), 0, s, a);
     } else {  // wide kernel half widths HC = 96 / 112 / 120
       if (ws)  // srbd_class_of routes every warm wide instance to class 7: one
                // warm instantiation at the full 128-column halves
