@@ -581,8 +581,8 @@ __device__ __forceinline__ void fill_k0k2(SrbdLds<W, NM> &S, int N, float Nf, in
 // Two-wave form: the same transposed write, one pivot half per wave (the
 // pivot column register is static inside each half), one s_barrier per
 // pivot, the pivot value through LDS.
-template <int H, int C2>
-__device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, Row<2> &K) {
+template <int H, int C2, int NM>
+__device__ __forceinline__ void invert_w2_half(SrbdLds<2, NM> &S, int t, int nw, Row<2> &K) {
   const int lane = t & 63;
   int nc = __builtin_amdgcn_readfirstlane(nw);
 #pragma unroll
@@ -608,8 +608,8 @@ __device__ __forceinline__ void invert_w2_half(SrbdLds<2> &S, int t, int nw, Row
   }
 }
 
-template <int C2>
-__device__ __forceinline__ void invert_w2(SrbdLds<2> &S, int t, const int (&ncol)[2], Row<2> &K) {
+template <int C2, int NM>
+__device__ __forceinline__ void invert_w2(SrbdLds<2, NM> &S, int t, const int (&ncol)[2], Row<2> &K) {
   invert_w2_half<0, C2>(S, t, ncol[0], K);
   // the buffer parity restarts with the second half (its first pivot may
   // reuse the buffer of the first half's last one): all reads of that
@@ -673,6 +673,12 @@ constexpr int kShortN = 10;
 #define QLOCO_SRBD_SHORT_WPE 4
 #endif
 constexpr int kShortWpe = QLOCO_SRBD_SHORT_WPE;
+// Two-wave C2 = 3 bucket for N <= kShortN (the mixed schedules' 21-25-leg
+// instances): waves per SIMD (0 disables the instantiation)
+#ifndef QLOCO_SRBD_W2_SHORT_WPE
+#define QLOCO_SRBD_W2_SHORT_WPE 4
+#endif
+constexpr int kW2ShortWpe = QLOCO_SRBD_W2_SHORT_WPE;
 #ifndef QLOCO_SRBD_NUM_VGPR_ATTR  // experiments: force a VGPR budget
 #define QLOCO_SRBD_NUM_VGPR_ATTR
 #endif
@@ -1547,8 +1553,8 @@ struct SrbdScratch {
   int *lists = nullptr;
   int *counts = nullptr;
   int64_t cap = 0;
-  hipStream_t side[2] = {nullptr, nullptr};
-  hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
 };
 static std::mutex g_srbd_scratch_mu;
 static std::map<std::pair<int, hipStream_t>, SrbdScratch> g_srbd_scratch;
@@ -1573,7 +1579,7 @@ static int srbd_scratch(int64_t batch, hipStream_t st, SrbdScratch **out) {
   }
   if (fresh) {
     if (hipMalloc(&s.counts, 8 * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 3; ++k) {
       if (hipStreamCreateWithFlags(&s.side[k], hipStreamNonBlocking) != hipSuccess) return QLOCO_ERR_DEVICE;
       if (hipEventCreateWithFlags(&s.join[k], hipEventDisableTiming) != hipSuccess) return QLOCO_ERR_DEVICE;
     }
@@ -1700,6 +1706,9 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
       if (ws)  // srbd_class_of routes every warm two-wave instance to bucket 4
         hipLaunchKernelGGL((srbd_admm_kernel<2, WP, true, kMaxN, 15>), grid, dim3(128), 0, s, a);
       // the narrow buckets fit 168 VGPRs: three waves per SIMD
+      else if (cls == 1 && a.N <= kShortN && kW2ShortWpe > 0)
+        // N <= 10: per-step LDS tables for N <= 10 (17 KB per workgroup)
+        hipLaunchKernelGGL((srbd_admm_kernel<2, (kW2ShortWpe > 0 ? kW2ShortWpe : 1), false, kShortN, 3>), grid, dim3(128), 0, s, a);
       else if (cls == 1)
         hipLaunchKernelGGL((srbd_admm_kernel<2, 3, false, kMaxN, 3>), grid, dim3(128), 0, s, a);
       else if (cls == 2)
@@ -1736,22 +1745,24 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
     QLOCO_HIP_CHECK(hipGetLastError(), "srbd_classify_kernel launch");
     const bool fork = srbd_fork_enabled();
     if (fork) QLOCO_HIP_CHECK(hipEventRecord(sc->fork, st), "fork event");
-    // class 0 on the caller's stream, the two-wave buckets in order on side
-    // stream 0, the wide buckets in order on side stream 1
-    bool waited[2] = {false, false};
-    int last[2] = {-1, -1};
+    // class 0 on the caller's stream; two-wave buckets 1 / 3 on side stream
+    // 0 and 2 / 4 on side stream 1 (a bucket's tail overlaps the next one's
+    // bulk); the wide buckets in order on side stream 2
+    bool waited[3] = {false, false, false};
+    int last[3] = {-1, -1, -1};
+    auto side_of = [](int c) { return c >= 5 ? 2 : ((c & 1) ? 0 : 1); };
     auto skip = [&](int c) {  // empty by construction (srbd_class_of)
       return ws && ((c >= 1 && c <= 3) || c == 5 || c == 6);
     };
     for (int c = 0; c <= top; ++c)
-      if (c > 0 && !skip(c)) last[c >= 5 ? 1 : 0] = c;
+      if (c > 0 && !skip(c)) last[side_of(c)] = c;
     for (int c = 0; c <= top; ++c) {
       if (skip(c)) continue;
       a.list = sc->lists + (int64_t)c * sc->cap;
       a.count = sc->counts + c;
       a.leg_lo = 0;
       a.leg_hi = 1 << 30;
-      const int sd = c >= 5 ? 1 : 0;
+      const int sd = side_of(c);
       hipStream_t s = st;
       if (fork && c > 0) {
         s = sc->side[sd];
