@@ -268,15 +268,13 @@ def main():
         if ev is not None:
             ev[0].record(stream)
         solver.solve(d_x0, d_xr, d_ft, d_ct, out=o, max_legs=legs, stream=stream.cuda_stream)
-        if ev is not None:
+        if ev is not None and ev[1] is not None:
             ev[1].record(stream)
         if gather is not None:
             if overlap:
                 _, pending[i % 2] = gather[i % 2](o.u0, async_op=True)
             else:
                 gather[0](o.u0)
-        if ev is not None:
-            ev[2].record(stream)
 
     def drain():
         for k in range(2):
@@ -290,16 +288,23 @@ def main():
     torch.cuda.synchronize(dev)
 
     K = args.steps
-    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    ev_k = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    # One timing event per step boundary (ev_b[i] starts step i, ev_b[K] ends
+    # the last), plus one after the solve only when an all-gather follows it:
+    # every event record costs the stream 2.5-5 us (tools/event_overhead.py,
+    # profiles/r3_event_overhead.txt), so the timed loop records no more
+    # than the numbers below need.  Without a gather, a step's span is its
+    # solve launch.
+    ev_b = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1)]
+    ev_k = [torch.cuda.Event(enable_timing=True) if gather is not None else None
+            for _ in range(K)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(K):
-        step(i, (ev_s[i], ev_k[i], ev_e[i]))
+        step(i, (ev_b[i], ev_k[i]))
     drain()
+    ev_b[K].record(stream)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -310,9 +315,13 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    kern_ms = np.array([ev_s[i].elapsed_time(ev_k[i]) for i in range(K)])
-    step_ms = np.array([ev_s[i].elapsed_time(ev_e[i]) for i in range(K)])
-    gather_ms = np.array([ev_k[i].elapsed_time(ev_e[i]) for i in range(K)])
+    step_ms = np.array([ev_b[i].elapsed_time(ev_b[i + 1]) for i in range(K)])
+    if gather is not None:
+        kern_ms = np.array([ev_b[i].elapsed_time(ev_k[i]) for i in range(K)])
+        gather_ms = np.array([ev_k[i].elapsed_time(ev_b[i + 1]) for i in range(K)])
+    else:
+        kern_ms = step_ms
+        gather_ms = np.zeros(K)
 
     # per-instance stats of the solved batch (identical every step)
     status = out.status.cpu().numpy()

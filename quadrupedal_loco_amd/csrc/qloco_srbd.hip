@@ -679,6 +679,14 @@ constexpr int kShortWpe = QLOCO_SRBD_SHORT_WPE;
 #define QLOCO_SRBD_W2_SHORT_WPE 4
 #endif
 constexpr int kW2ShortWpe = QLOCO_SRBD_W2_SHORT_WPE;
+// Two-wave C2 = 6 bucket for N <= kShortN (the mixed schedules' 26-29-leg
+// instances): waves per SIMD (0: the kMaxN three-wave instantiation).
+// Four waves (128 VGPRs, 56 spilled, 17 KB LDS): mixed config-5 share
+// 16.61-16.63 vs 16.73-16.77 ms same-call (profiles/r3_c6_wpe4_ab.txt)
+#ifndef QLOCO_SRBD_W2_C6_SHORT_WPE
+#define QLOCO_SRBD_W2_C6_SHORT_WPE 4
+#endif
+constexpr int kW2C6ShortWpe = QLOCO_SRBD_W2_C6_SHORT_WPE;
 #ifndef QLOCO_SRBD_NUM_VGPR_ATTR  // experiments: force a VGPR budget
 #define QLOCO_SRBD_NUM_VGPR_ATTR
 #endif
@@ -1711,6 +1719,8 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
         hipLaunchKernelGGL((srbd_admm_kernel<2, (kW2ShortWpe > 0 ? kW2ShortWpe : 1), false, kShortN, 3>), grid, dim3(128), 0, s, a);
       else if (cls == 1)
         hipLaunchKernelGGL((srbd_admm_kernel<2, 3, false, kMaxN, 3>), grid, dim3(128), 0, s, a);
+      else if (cls == 2 && a.N <= kShortN && kW2C6ShortWpe > 0)
+        hipLaunchKernelGGL((srbd_admm_kernel<2, (kW2C6ShortWpe > 0 ? kW2C6ShortWpe : 1), false, kShortN, 6>), grid, dim3(128), 0, s, a);
       else if (cls == 2)
         hipLaunchKernelGGL((srbd_admm_kernel<2, 3, false, kMaxN, 6>), grid, dim3(128), 0, s, a);
       else if (cls == 3)
