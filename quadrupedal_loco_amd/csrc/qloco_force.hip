@@ -150,8 +150,13 @@ __device__ __forceinline__ void force_distribution(const double *com_des, const 
   for (int k = 0; k < 12; ++k) R[k] = mode == 101 ? p1[k] : (mode == 102 ? p2[k] : R[k]);
 }
 
-#ifndef QLOCO_FORCE_WPE  // waves per SIMD the register budget targets
-#define QLOCO_FORCE_WPE 3
+// Waves per SIMD the register budget targets.  Two: 239 VGPRs, no scratch.
+// Three (168 VGPRs) was 1.5 % faster (0.721 vs 0.734 ms at 65,536 robots)
+// but spills 96 VGPRs -- 340 B of scratch per lane, 370 MB of HBM writes per
+// launch against 58 MB of algorithmic traffic (profiles/r3ft_traffic_force_
+// qp_b65536_wpe3.json) -- so the spill-free budget is the shipped one.
+#ifndef QLOCO_FORCE_WPE
+#define QLOCO_FORCE_WPE 2
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_WPE))) void force_qp_kernel(
     const ForceArgs a) {
