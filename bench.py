@@ -379,7 +379,8 @@ def main():
                      "closed-form Hessian removes the B'QB GEMM, DESIGN.md 3); peak = FP32 vector "
                      "157.3 TF.  achieved / frac count SURVEY.md 8(d)'s ALGORITHMIC flops of the "
                      "reference's 12N-variable QP (%.3g per launch) / mean kernel time (HIP events "
-                     "on the launch stream)%s; executed / executed_frac = the flops this kernel "
+                     "on the launch stream, one per step boundary: without an all-gather a "
+                     "step's span is its solve launch)%s; executed / executed_frac = the flops this kernel "
                      "actually performs (%.3g per launch, DESIGN.md 5) -- the number that rates "
                      "the kernel" % (flops_alg, "" if args.literal else
                                      ", which the stance-only kernel never builds", flops_exec)),

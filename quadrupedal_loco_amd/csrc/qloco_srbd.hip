@@ -675,16 +675,21 @@ constexpr int kShortN = 10;
 constexpr int kShortWpe = QLOCO_SRBD_SHORT_WPE;
 // Two-wave C2 = 3 bucket for N <= kShortN (the mixed schedules' 21-25-leg
 // instances): waves per SIMD (0 disables the instantiation)
+// 0 (shipped): at four waves per SIMD (128 VGPRs) the bucket spills inside
+// the ADMM loop -- 1.36 GB of scratch writes per mixed config-5 share launch
+// against 15 MB at three waves, for 1 % of time (profiles/r3wt_*)
 #ifndef QLOCO_SRBD_W2_SHORT_WPE
-#define QLOCO_SRBD_W2_SHORT_WPE 4
+#define QLOCO_SRBD_W2_SHORT_WPE 0
 #endif
 constexpr int kW2ShortWpe = QLOCO_SRBD_W2_SHORT_WPE;
 // Two-wave C2 = 6 bucket for N <= kShortN (the mixed schedules' 26-29-leg
 // instances): waves per SIMD (0: the kMaxN three-wave instantiation).
 // Four waves (128 VGPRs, 56 spilled, 17 KB LDS): mixed config-5 share
-// 16.61-16.63 vs 16.73-16.77 ms same-call (profiles/r3_c6_wpe4_ab.txt)
+// 16.61-16.63 vs 16.73-16.77 ms same-call (profiles/r3_c6_wpe4_ab.txt), but
+// 1.31 GB of spill writes per launch against 15 MB at three waves
+// (profiles/r3wt_w2_bucket_traffic_mixed.txt): 0, the spill-free-loop form, ships
 #ifndef QLOCO_SRBD_W2_C6_SHORT_WPE
-#define QLOCO_SRBD_W2_C6_SHORT_WPE 4
+#define QLOCO_SRBD_W2_C6_SHORT_WPE 0
 #endif
 constexpr int kW2C6ShortWpe = QLOCO_SRBD_W2_C6_SHORT_WPE;
 #ifndef QLOCO_SRBD_NUM_VGPR_ATTR  // experiments: force a VGPR budget
