@@ -151,6 +151,13 @@ int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, const float 
                         int32_t *rho_updates, float *obj, float *warm,
                         int32_t max_stance_legs, void *stream);
 
+/* Class-dispatch scratch of qloco_srbd_solve_ex (instance lists, counters,
+ * side streams, events): one set per (device, caller stream), at most 8
+ * live -- the least recently used set beyond that is released.  Returns the
+ * live sets; *pinned (may be NULL) = allocations kept for the life of the
+ * process because a stream capture baked them into a graph. */
+int qloco_srbd_scratch_sets(int32_t *pinned);
+
 /* Batched condensed-QP build only (ConvexMpc::calculate_qp_mats, dense,
  * as the reference materialises it).  Outputs per instance (NULL = skip):
  *   H[B*(12N)^2] col-major, g[B*12N], lb[B*20N], ub[B*20N] (+-1e30 = INFTY),
@@ -194,8 +201,14 @@ int qloco_eiquadprog_solve(int32_t n, int32_t p, int32_t m, int64_t batch, const
                            int64_t ce0_stride, const double *CI, int64_t CI_stride,
                            const double *ci0, int64_t ci0_stride, double *x, double *f,
                            int32_t *status, int32_t *iters, void *stream);
+/* the largest n of the fast path (four QPs per wavefront, bit-exact in the */
+/* common case): 16 -- unchanged since round 1; sizes above it up to        */
+/* qloco_gi_limits run one QP per wavefront                                 */
 int qloco_max_gi_vars(void);
-/* the size limits above: n, p, m (any pointer may be NULL) */
+/* the fast path's limits n, p, m (16, 16, 64; any pointer may be NULL)    */
+void qloco_gi_fast_limits(int32_t *n, int32_t *p, int32_t *m);
+/* the size limits above (QPBaseClass's capacity rounded up): n, p, m      */
+/* (64, 64, 320; any pointer may be NULL)                                   */
 void qloco_gi_limits(int32_t *n, int32_t *p, int32_t *m);
 
 /* ====================================================================== */

@@ -76,6 +76,8 @@ SIGNATURES = {
                                          vp, i64, vp, i64, vp, vp, vp, vp, vp]),
     "qloco_max_gi_vars": (C.c_int, []),
     "qloco_gi_limits": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "qloco_gi_fast_limits": (None, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "qloco_srbd_scratch_sets": (C.c_int, [C.c_void_p]),
     "qloco_force_params_default": (None, [C.POINTER(ForceParams)]),
     "qloco_force_qp_solve": (C.c_int, [C.POINTER(ForceParams), i64] + [vp] * 18),
     "qloco_leg_fk": (C.c_int, [i64] + [vp] * 7),

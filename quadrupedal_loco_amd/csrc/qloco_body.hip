@@ -294,14 +294,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
     GI_SYNC();
     double f;
     int it;
-#ifndef QLOCO_ABLATE_BODY_GI
     gi_solve_group(P.gi, li, BNT, 0, BNI, P.gi.R, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
                    status, it);
-#else  // timing experiments only (tools/variant_lib.py): setup + outputs without the solve
-    if (li < BNT) P.x[li] = P.g0[li] * 1e-9;
-    f = 0.0;
-    it = 0;
-#endif
     GI_SYNC();
     if (li == 0) {
       bool ok = true;

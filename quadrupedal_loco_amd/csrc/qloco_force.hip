@@ -155,10 +155,8 @@ __device__ __forceinline__ void force_distribution(const double *com_des, const 
 // but spills 96 VGPRs -- 340 B of scratch per lane, 370 MB of HBM writes per
 // launch against 58 MB of algorithmic traffic (profiles/r3ft_traffic_force_
 // qp_b65536_wpe3.json) -- so the spill-free budget is the shipped one.
-#ifndef QLOCO_FORCE_WPE
-#define QLOCO_FORCE_WPE 2
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_WPE))) void force_qp_kernel(
+constexpr int kForceWpe = 2;
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kForceWpe))) void force_qp_kernel(
     const ForceArgs a) {
   __shared__ ForceLds S;
   const int lane = threadIdx.x, grp = lane >> 4, li = lane & 15;
@@ -226,16 +224,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QLOCO_FORCE_
   }
   double f;
   int st, it;
-#ifndef QLOCO_ABLATE_FORCE_GI
   gi_solve_group(P.gi, li, 12, 12, 24, PG, 12, P.g0, c_force_CE[pat], c_force_zeros,
                  ForceCi{a.mu, a.fz_max}, P.gi.x,
                  f, st, it);
-#else  // timing experiments only (tools/variant_lib.py): everything but the solve
-  if (li < 12) P.gi.x[li] = P.g0[li] * 1e-9;
-  f = 0.0;
-  st = 0;
-  it = pat;
-#endif
   GI_SYNC();
   // QPBaseClass::solveQP: success iff no NaN (go1_rt_control QPBaseClass.cpp:116-142); Solve / fallback
   bool ok = true;
@@ -379,9 +370,3 @@ extern "C" int qloco_joint_torques(int64_t batch, const double *Jaco, const int3
   return QLOCO_OK;
 }
 
-#ifdef QLOCO_GI_PHASE_TIMING
-extern "C" int qloco_gi_phase_read(unsigned int *host, size_t count) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(qloco::g_gi_phase), count * sizeof(unsigned int), 0,
-                                  hipMemcpyDeviceToHost);
-}
-#endif

@@ -52,7 +52,15 @@ __global__ __launch_bounds__(64) void gi_kernel(const GiArgs a) {
 
 using namespace qloco;
 
-extern "C" int qloco_max_gi_vars(void) { return kGiWideN; }
+// the fast path's variable limit (four QPs per wavefront, gi_kernel) -- what
+// this query has always meant; the capacity limits are qloco_gi_limits
+extern "C" int qloco_max_gi_vars(void) { return GI_N; }
+
+extern "C" void qloco_gi_fast_limits(int32_t *n, int32_t *p, int32_t *m) {
+  if (n) *n = GI_N;
+  if (p) *p = GI_P;
+  if (m) *m = GI_M;
+}
 
 extern "C" void qloco_gi_limits(int32_t *n, int32_t *p, int32_t *m) {
   if (n) *n = kGiWideN;

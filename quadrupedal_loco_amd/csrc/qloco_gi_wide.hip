@@ -27,6 +27,7 @@
 #include <float.h>
 #include <math.h>
 #include <string.h>
+#include <mutex>
 
 #include "qloco_common.hpp"
 #include "qloco_gi_wide.hpp"
@@ -638,12 +639,29 @@ int gi_wide_launch(int n, int p, int m, int64_t batch, const double *G, int64_t 
   a.status = status;
   a.iters = iters;
   const size_t lds = gw_lds_bytes(n, p, m);
-  static const bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(gi_wide_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==
-           hipSuccess;
-  }();
-  (void)attr;
+  // dynamic LDS beyond the 64 KB default needs the attribute, set once per
+  // device; a device that refuses it cannot run the larger shapes, and the
+  // caller is told why instead of getting a generic launch failure
+  if (lds > 64 * 1024) {
+    static std::mutex mu;
+    static int state[64] = {0};  // per device: 0 unknown, 1 set, -1 refused
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return QLOCO_ERR_DEVICE;
+    std::lock_guard<std::mutex> lk(mu);
+    if (state[dev] == 0) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(gi_wide_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      state[dev] = e == hipSuccess ? 1 : -1;
+      if (e != hipSuccess) {
+        set_last_error("gi_wide_kernel: the device refused 160 KB of dynamic LDS "
+                       "(hipFuncAttributeMaxDynamicSharedMemorySize); shapes needing more than "
+                       "64 KB cannot run",
+                       e);
+        (void)hipGetLastError();
+      }
+    }
+    if (state[dev] < 0) return QLOCO_BAD_SIZE;
+  }
   hipLaunchKernelGGL(gi_wide_kernel, dim3((unsigned)batch), dim3(64), lds, stream, a);
   QLOCO_HIP_CHECK(hipGetLastError(), "gi_wide_kernel launch");
   return QLOCO_OK;

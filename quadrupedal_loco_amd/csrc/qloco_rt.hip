@@ -647,9 +647,7 @@ __global__ __launch_bounds__(PRE_T) void rt_pre_kernel(const RtArgs a) {
       for (int k = 1; k < 25; ++k) R.D(F_NRT + k) = ctrl[k];
       if (walk) {
         R.I(I_MPC) = mpc;
-#ifndef QLOCO_ABLATE_RT_INTERP  // timing experiments only (tools/gpu_rt_ablate.sh)
         interpolation(a, R, g, flag, t_int, t_end);
-#endif
         R.D(F_ZMP + 8) = 0.0;  // zmpxyz_ref(2) = _Zsc = {l,r}foot_inter(2) = 0 (:557-566)
         *(reinterpret_cast<int32_t *>(a.ws + L.bi) + r) = mpc;
       }
@@ -662,12 +660,8 @@ __global__ __launch_bounds__(PRE_T) void rt_pre_kernel(const RtArgs a) {
     const int foot_i = (int)(mpc - (int)1.0 / DT_FAST);
     int bjx1 = (int)body[26], bjxx = R.I(I_BJXX), te = t_end;
     int sxx[NH], sx1[NH];
-#ifndef QLOCO_ABLATE_RT_FOOT  // timing experiments only
     foot_traj_mod2(R, foot_i, nrt, bjx1, bjxx, te, sxx, sx1);
-#ifndef QLOCO_ABLATE_RT_ROT
     foot_rotation(R, foot_i, bjx1, bjxx, te, sxx, sx1);
-#endif
-#endif
     body[26] = bjx1;
     R.I(I_BJXX) = bjxx;
     R.I(I_TEND) = te;
@@ -680,7 +674,6 @@ __global__ __launch_bounds__(PRE_T) void rt_pre_kernel(const RtArgs a) {
   }
   // the reference record of every robot (read by body_mpc_kernel only where
   // run = 1), written row-coalesced; the two waves take alternate slots
-#ifndef QLOCO_ABLATE_RT_REF  // timing experiments only
   double *ref = reinterpret_cast<double *>(a.ws + L.ref);
 #pragma unroll
   for (int c0 = 0; c0 < RF_USED; c0 += STG_C) {
@@ -696,7 +689,6 @@ __global__ __launch_bounds__(PRE_T) void rt_pre_kernel(const RtArgs a) {
     }
     __syncthreads();
   }
-#endif
 }
 
 // /rtMPC/traj slot k in [36, 100) of robot R: low_mpc_gait_inte(k - 36)

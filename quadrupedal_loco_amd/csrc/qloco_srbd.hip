@@ -21,14 +21,18 @@
 //  * ADMM is OSQP's algorithm (Ruiz scaling, rho vector, relaxation,
 //    termination every check_termination iterations, adaptive rho) in fp32.
 //    Lane v owns stance variable v (leg triples never straddle a wave:
-//    21 legs = 63 lanes per wave, lane 63 pads), its row of K^-1 in 32*W
-//    packed-fp32 VGPR pairs (K = P + sigma I + A' diag(rho) A, inverted in
+//    21 legs = 63 lanes per wave, lane 63 pads), its row of K^-1 in up to
+//    64*W VGPRs (K = P + sigma I + A' diag(rho) A, inverted in
 //    place by Gauss-Jordan), and the <= 2 constraint rows of its leg's 5
-//    (x: rows 0,1; y: rows 2,3; z: row 4).  Padding rows/columns are the
-//    identity, so every loop over columns is straight-line code.
-//    Per iteration: one LDS broadcast of the KKT right-hand side, one
-//    packed-FMA matvec against the register-resident K^-1, four DPP lane
-//    shifts (wave_shr/wave_shl) for the leg-local constraint couplings.
+//    (x: rows 0,1; y: rows 2,3; z: row 4).  Padding lanes carry zero A rows,
+//    zero q and so a zero right-hand side; their K rows are the identity row
+//    where the diagonal falls inside the columns a form keeps (NK), a zero
+//    row past it (the narrowed forms allocate no padding columns), and either
+//    way their x_tilde is 0 -- every loop over columns is straight-line code.
+//    Per iteration: one LDS broadcast of the KKT right-hand side, one matvec
+//    against the register-resident K^-1 (one v_fmac_f32_dpp row_newbcast per
+//    entry, qloco_dpp.inc), DPP lane shifts (wave_shr/wave_shl) for the
+//    leg-local constraint couplings.
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -58,10 +62,7 @@ constexpr int kLegsPerWave = 21;
 // kernel carry a single 60-column form of its inverse, matvec and Ruiz
 // sweeps -- 124 -> ~80 KB of code; 21-leg instances then go to the two-wave
 // class.  21 keeps the 64-column forms as well.
-#ifndef QLOCO_W1_LEGS
-#define QLOCO_W1_LEGS 20
-#endif
-constexpr int kW1Legs = QLOCO_W1_LEGS;
+constexpr int kW1Legs = 20;
 static_assert(kW1Legs == 20 || kW1Legs == 21, "one-wave class: 20 or 21 legs");
 
 struct SrbdArgs {
@@ -252,9 +253,6 @@ __device__ __forceinline__ float bqp_t(const SrbdLds<W, NM> &S, int step, int co
 template <int W, int NM>
 __device__ __forceinline__ void row_scans(SrbdLds<W, NM> &S, int N, bool forward) {
   const int r = threadIdx.x;
-#ifdef QLOCO_ABLATE_NO_SCAN  // timing experiments only
-  if (forward) return;
-#endif
   if (r >= 12) return;
   const bool brow = r >= 6;
   float v[NM];
@@ -365,15 +363,11 @@ __device__ __forceinline__ float p_times_x(SrbdLds<W, NM> &S, int N, bool valid,
     S.err[idx] = acc;
   }
   bsync<W>();
-#ifndef QLOCO_PX_SCANS
   if (N == 10) {
     horizon_rows<W, 10>(S, N);
   } else {
     horizon_rows<W, 0>(S, N);
   }
-#else
-  row_scans<W>(S, N, true);
-#endif
   bsync<W>();
   return valid ? bqp_t<W>(S, step, comp, lo, hi, dtm, dt2m) + r2v * xu : 0.0f;
 }
@@ -528,8 +522,9 @@ __device__ __forceinline__ float finalize_row(const SrbdLds<W, NM> &S, int t, in
 // processed c (< k), so every lane writes its own column-k entry as the pivot
 // row (a static register: the pivot loop is unrolled) and the pivot is a
 // v_readlane -- one coalesced ds_write_b32 and one ds_read_b128 per pivot,
-// the row fanned out by DPP.  Only the valid pivots run; padding rows /
-// columns are the identity and never change.
+// the row fanned out by DPP.  Only the valid pivots run; padding rows never
+// change: identity rows inside the kept columns, zero rows past them (the
+// narrowed forms stop at NK), both with a zero right-hand side.
 constexpr float kGjExactPivot = 16.0f;
 
 template <bool C60, int NM>
@@ -619,82 +614,26 @@ __device__ __forceinline__ void invert_w2(SrbdLds<2, NM> &S, int t, const int (&
   __syncthreads();
 }
 
-// Development-only phase timing (tools/phase_timing.py builds a separate
-// library with -DQLOCO_PHASE_TIMING; the product build never defines it).
-#ifdef QLOCO_TRACE_SIMD
-__device__ unsigned int g_trace[4 << 18];
-#endif
-#ifdef QLOCO_PHASE_TIMING
-__device__ unsigned int g_phase[1 << 20];
-#define QL_PHASE(i)                                                           \
-  do {                                                                        \
-    const uint64_t _now = __builtin_readcyclecounter();                       \
-    if (t == 0 && b < (1 << 16)) g_phase[b * 16 + (i)] = (unsigned)(_now - _t0); \
-  } while (0)
-// sub-phase accumulators (slots 9..15), reset at kernel entry
-#define QL_PSTAMP(v) const uint64_t v = __builtin_readcyclecounter()
-#define QL_PACC(i, v0)                                                              \
-  do {                                                                              \
-    const uint64_t _n = __builtin_readcyclecounter();                               \
-    if (t == 0 && b < (1 << 16)) g_phase[b * 16 + (i)] += (unsigned)(_n - (v0));   \
-  } while (0)
-#else
-#define QL_PHASE(i) ((void)0)
-#define QL_PSTAMP(v) ((void)0)
-#define QL_PACC(i, v0) ((void)0)
-#endif
 
-#ifndef QLOCO_SRBD_W2_C9_WPE  // occupancy of the C2 = 9 two-wave bucket (30-33 legs, N = 16 trot)
-#define QLOCO_SRBD_W2_C9_WPE 3
-#endif
-#ifndef QLOCO_SRBD_W2_C15_WPE  // occupancy of the C2 = 15 two-wave bucket (34-41 legs, N = 20 pace)
-#define QLOCO_SRBD_W2_C15_WPE 3
-#endif
-#ifndef QLOCO_SRBD_WAVES_PER_EU_W2  // two-wave kernel occupancy
-#define QLOCO_SRBD_WAVES_PER_EU_W2 2
-#endif
-#ifndef QLOCO_SRBD_WAVES_PER_EU  // one-wave kernel occupancy for large batches: 3 waves/SIMD
-#define QLOCO_SRBD_WAVES_PER_EU 3    // = 168 VGPRs (small spills, all in setup / refactor paths)
-#endif
-// One-wave kernel, small batches (<= kSmallBatch instances, i.e. <= 6 waves
-// per SIMD over the launch): 2 waves/SIMD = 186 VGPRs, spill-free -- with few
-// waves per SIMD the tail of long instances dominates and more registers per
-// wave (no scratch round trips) beat the third resident wave.  Measured on
-// Go1 trot N = 10 (same-call pairs, profiles/r2ab_*, r2v_*): B = 4096 306-307
-// vs 310-314 us, B = 8192 539-555 vs 487-499 us.
-#ifndef QLOCO_SMALL_BATCH
-#define QLOCO_SMALL_BATCH 6144
-#endif
-constexpr int64_t kSmallBatch = QLOCO_SMALL_BATCH;
-// One-wave kernel for horizons N <= kShortN: LDS tables sized for kShortN,
-// QLOCO_SRBD_SHORT_WPE waves per SIMD (0 disables the instantiation).
+// Occupancy (waves per SIMD, amdgpu_waves_per_eu) of each instantiation,
+// every choice a same-call A/B:
+//  * one-wave kernel, N <= kShortN: per-step LDS tables sized for N <= 10
+//    (9 KB) and four waves per SIMD (128 VGPRs) -- all 4096 headline
+//    instances resident from the first cycle (profiles/r3_occ_ab.txt);
+//  * one-wave kernel, longer horizons: three waves (168 VGPRs, small spills
+//    in the setup / refactor paths) above kSmallBatch instances, two waves
+//    (186 VGPRs, spill-free) at or below it -- with few waves per SIMD the
+//    tail of long instances dominates (profiles/r2ab_*, r2v_*);
+//  * two-wave buckets C2 = 3 / 6 / 9 / 15: three waves; the C2 = 3 / 6
+//    buckets at four waves for N <= 10 were 1.5 % faster but spilled inside
+//    the ADMM loop (1.36 / 1.31 GB of scratch writes per mixed launch,
+//    profiles/r3wt_*), so they are not instantiated;
+//  * warm-started two-wave instances: one C2 = 15 instantiation at two waves.
 constexpr int kShortN = 10;
-#ifndef QLOCO_SRBD_SHORT_WPE
-#define QLOCO_SRBD_SHORT_WPE 4
-#endif
-constexpr int kShortWpe = QLOCO_SRBD_SHORT_WPE;
-// Two-wave C2 = 3 bucket for N <= kShortN (the mixed schedules' 21-25-leg
-// instances): waves per SIMD (0 disables the instantiation)
-// 0 (shipped): at four waves per SIMD (128 VGPRs) the bucket spills inside
-// the ADMM loop -- 1.36 GB of scratch writes per mixed config-5 share launch
-// against 15 MB at three waves, for 1 % of time (profiles/r3wt_*)
-#ifndef QLOCO_SRBD_W2_SHORT_WPE
-#define QLOCO_SRBD_W2_SHORT_WPE 0
-#endif
-constexpr int kW2ShortWpe = QLOCO_SRBD_W2_SHORT_WPE;
-// Two-wave C2 = 6 bucket for N <= kShortN (the mixed schedules' 26-29-leg
-// instances): waves per SIMD (0: the kMaxN three-wave instantiation).
-// Four waves (128 VGPRs, 56 spilled, 17 KB LDS): mixed config-5 share
-// 16.61-16.63 vs 16.73-16.77 ms same-call (profiles/r3_c6_wpe4_ab.txt), but
-// 1.31 GB of spill writes per launch against 15 MB at three waves
-// (profiles/r3wt_w2_bucket_traffic_mixed.txt): 0, the spill-free-loop form, ships
-#ifndef QLOCO_SRBD_W2_C6_SHORT_WPE
-#define QLOCO_SRBD_W2_C6_SHORT_WPE 0
-#endif
-constexpr int kW2C6ShortWpe = QLOCO_SRBD_W2_C6_SHORT_WPE;
-#ifndef QLOCO_SRBD_NUM_VGPR_ATTR  // experiments: force a VGPR budget
-#define QLOCO_SRBD_NUM_VGPR_ATTR
-#endif
+constexpr int kShortWpe = 4;
+constexpr int kW1Wpe = 3, kW1SmallWpe = 2;
+constexpr int64_t kSmallBatch = 6144;
+constexpr int kW2Wpe = 3, kW2WarmWpe = 2;
 
 // WS: a warm-start mode (1 or 2) may be set.  The cold-start instantiation
 // (the headline path) carries none of the warm / persistent-record code.
@@ -704,11 +643,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
   constexpr int NK = W == 1 ? (kW1Legs <= 20 ? 60 : 64) : 64 + 4 * C2;  // register columns of K in use
   const int t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
-#ifdef QLOCO_PHASE_TIMING
-  const uint64_t _t0 = __builtin_readcyclecounter();
-  if (t == 0 && b < (1 << 16))
-    for (int i = 9; i < 16; ++i) g_phase[b * 16 + i] = 0;
-#endif
   const int N = a.N;
   const float Nf = (float)N;
   const float dt = a.dt;
@@ -801,7 +735,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
   S.cst[t] = valid ? step : NM;
   fill_k0k2<W>(S, N, Nf, t);
 
-  QL_PHASE(1);
   // ---------------- 3. SRBD model terms (ConvexMpc.cpp:111-160, compute_grf :502-549)
   const float yaw = S.x0[2];
   const float cy = cosf(yaw), sy = sinf(yaw);
@@ -890,7 +823,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
   float qsv = qv;
   if (p_same) qsv = valid ? prec[84 * N + 12 * step + 3 * leg + comp] : 0.0f;
 
-  QL_PHASE(2);
   // ---------------- 5. constraint rows owned by this lane (ConvexMpc.cpp:47-59, :227-249)
   //  x lane: rows 0 [1,0, mu] in [0,inf), 1 [1,0,-mu] in (-inf,0]
   //  y lane: rows 2 [0,1, mu] in [0,inf), 3 [0,1,-mu] in (-inf,0]
@@ -956,12 +888,8 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
     S.xs[t] = valid ? x * Drl : 0.0f;
     bsync<W>();
     const f4v blo = S.bv[t][0], bhi = S.bv[t][1];
-#ifdef QLOCO_ABLATE_NO_PX  // timing experiments only
-    const float pxo = x * Drl;
-#else
     const float pxo = p_times_x<W>(S, N, valid, (int)bhi.z, comp, blo, bhi, S.aux[0][t], x * Drl,
                                    dtm, dt2m);
-#endif
     const float Dinv = __builtin_amdgcn_rcpf(Drl);
     const f2v Einv = {__builtin_amdgcn_rcpf(S.aux[1][t]), __builtin_amdgcn_rcpf(S.aux[2][t])};
     const f4v arz = S.arz[t];
@@ -1007,7 +935,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       gen_p_row<W, C2>(S, pc, t, valid, (int)bhi.z, comp, S.aux[0][t], K);
     }
     if (first) {
-      QL_PHASE(3);
       // ---------------- 7. modified Ruiz equilibration (OSQP scaling.c); K
       // keeps the unscaled P, row norms of the scaled P = cs D P D come from
       // the DPP-fanned D chunk
@@ -1016,7 +943,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       for (int c = 0; c < NK; ++c) cnP = fmaxf(cnP, fabsf(KE(K, c)));
       const float inv_n = 1.0f / (float)(n > 0 ? n : 1);
       for (int it = 0; it < a.scaling; ++it) {
-        QL_PSTAMP(_r0);
         float cnA = fmaxf(fabsf(ra0), fabsf(ra1));
         const float zmax = fmaxf(fabsf(rz0), fabsf(rz1));
         const float zm1 = lane_prev(zmax), zm2 = lane_prev(zm1);
@@ -1041,8 +967,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         reinterpret_cast<float *>(&S.bc[buf][0])[t] = Dr;
         bsync<W>();
         float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f, t0, t1, t2, t3;
-        QL_PACC(9, _r0);
-        QL_PSTAMP(_r1);
         {
           const f4v d0 = S.bc[buf][lane & 15];
           if (W == 1 && c60) {  // padding columns: K_rc = 0 on valid rows
@@ -1058,8 +982,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         }
         // row norm of D P D after this pass (without the running cost scale)
         const float cn2 = Dr * fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
-        QL_PACC(10, _r1);
-        QL_PSTAMP(_r2);
         // cost scaling: mean column norm of P (= row norm, P symmetric) vs ||q||_inf
         const float sumP = bsum<W>(valid ? cn2 : 0.0f, S.red);
         float qm[1] = {valid ? fabsf(qsv) : 0.0f};
@@ -1071,7 +993,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         qsv *= ctc;
         cs *= ctc;
         cnP = cn2 * cs;
-        QL_PACC(11, _r2);
       }
       cinv = 1.0f / cs;
       const float lh0 = rl0 * rE0, uh0 = ru0 * rE0;
@@ -1093,35 +1014,16 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       S.arz[t] = (f4v){ra0, ra1, rz0, rz1};
       S.qs[t] = qv;
       bsync<W>();
-      QL_PHASE(4);
     }
     // ---------------- 8. K = cs D P D + sigma I + A' rho A, inverse in registers
     {
       float add0, add1, add2;
       leg_block(add0, add1, add2);
       const float dg = finalize_row<W, C2>(S, t, t - comp, cs * S.Dc[t], add0, add1, add2, c60, K);
-#ifdef QLOCO_DEBUG_INST
-      if (b == QLOCO_DEBUG_INST) {
-        float kd = 0.0f;
-        for (int c = 0; c < NC; ++c) kd = (c == t) ? K.k[c] : kd;
-        const uint64_t em = __ballot(eq0);
-        const int l0 = em ? __ffsll((long long)em) - 1 : 0;
-        const float kd0 = rlane(kd, l0), a20 = rlane(add2, l0), rv00 = rlane(RV0, l0),
-                    raz = rlane(S.arz[t].x, l0);
-        if (lane == 0)
-          printf("inst %d wave %d iter %d rho %g: eq lanes %d first eq lane %d RV0 %g add2 %g "
-                 "ra %g K diag %g\n", (int)b, wave, iter, rho, __popcll(em), l0, rv00, a20, raz, kd0);
-      }
-#endif
-      if (first) QL_PHASE(5);
       if constexpr (W == 1) {
         (void)dg;
         if (c60) {
           invert_w1<true>(S, t, ncol[0], K);
-#ifdef QLOCO_ABLATE_DUP_INV  // timing experiments only: K^-1 -> K -> K^-1
-          invert_w1<true>(S, t, ncol[0], K);
-          invert_w1<true>(S, t, ncol[0], K);
-#endif
         } else {
           invert_w1<false>(S, t, ncol[0], K);
         }
@@ -1129,23 +1031,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         (void)dg;
         invert_w2<C2>(S, t, ncol, K);
       }
-      if (first) QL_PHASE(6);
-#ifdef QLOCO_DEBUG_INST  // development only (tools/variant_lib.py): inverse health of one instance
-      if (b == QLOCO_DEBUG_INST) {
-        float mx = 0.0f, nf = 0.0f, dg = 0.0f;
-        for (int c = 0; c < NC; ++c) {
-          mx = fmaxf(mx, fabsf(K.k[c]));
-          nf += isfinite(K.k[c]) ? 0.0f : 1.0f;
-          dg = (c == t) ? K.k[c] : dg;
-        }
-        mx = wmax(mx);
-        nf = wsum(nf);
-        const float dmin = -wmax(valid ? -dg : -1e30f);
-        if (lane == 0)
-          printf("inst %d wave %d iter %d rho %g: K^-1 max %g nonfinite %g min diag %g\n", (int)b,
-                 wave, iter, rho, mx, nf, dmin);
-      }
-#endif
     }
     if (first) {
       first = false;
@@ -1227,15 +1112,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         {
           const f4v r0 = S.bc[buf][lane & 15];
           if constexpr (W == 1) {
-#ifdef QLOCO_MATVEC4  // four accumulator chains
-            float acc0, acc1, acc2, acc3;
-            if constexpr (C60) {
-              QL_DPP_MATVEC60(acc0, acc1, acc2, acc3, r0, K.k, 0);
-            } else {
-              QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r0, K.k, 0);
-            }
-            xt = (acc0 + acc1) + (acc2 + acc3);
-#else  // two accumulator chains
+            // two accumulator chains (four measured no faster)
             float acc0, acc1;
             if constexpr (C60) {
               QL_DPP_MATVEC60_2(acc0, acc1, r0, K.k, 0);
@@ -1243,7 +1120,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
               QL_DPP_MATVEC64_2(acc0, acc1, r0, K.k, 0);
             }
             xt = acc0 + acc1;
-#endif
           } else {
             float acc0, acc1, acc2, acc3;
             QL_DPP_MATVEC64(acc0, acc1, acc2, acc3, r0, K.k, 0);
@@ -1277,16 +1153,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
                         __builtin_amdgcn_fmed3f(v.y, bnd.z, bnd.w)};
         y = __builtin_elementwise_fma(rv, zr - zn, y);
         z = zn;
-#ifdef QLOCO_DEBUG_INST
-        if (b == QLOCO_DEBUG_INST && iter >= 95 && iter < 130) {
-          const float ax = wmax(fabsf(x)), az = wmax(fmaxf(fabsf(z.x), fabsf(z.y))),
-                      ay = wmax(fmaxf(fabsf(y.x), fabsf(y.y))), at = wmax(fabsf(xt)),
-                      ar = wmax(fabsf(rhs));
-          if (lane == 0)
-            printf("inst %d wave %d iter %d: |x| %g |z| %g |y| %g |xt| %g |rhs| %g\n", (int)b, wave,
-                   iter, ax, az, ay, at, ar);
-        }
-#endif
       }
       };
       if constexpr (W == 1) {
@@ -1344,7 +1210,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
     if (!refactor) break;
   }
 
-  QL_PHASE(7);
   // ---------------- 10. outputs: unscale, objective, scatter to leg slots
   const float Dr_o = S.Dc[t];
   const int pr_o = S.pair[t];
@@ -1414,7 +1279,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       if (xy) wy[rbase + 1] = cinv * S.aux[2][t] * y.y;
     }
   }
-  QL_PHASE(8);
   if (t == 0) {
     if (a.status) a.status[b] = status;
     if (a.iters) a.iters[b] = iter;
@@ -1427,24 +1291,12 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
 // list positions below the device-side count (or the batch).
 template <int W, int WPE, bool WS, int NM = kMaxN, int C2 = 16>
 __global__ __launch_bounds__(64 * W)
-__attribute__((amdgpu_waves_per_eu(WPE))) QLOCO_SRBD_NUM_VGPR_ATTR
+__attribute__((amdgpu_waves_per_eu(WPE)))
 void srbd_admm_kernel(const SrbdArgs a) {
   __shared__ __attribute__((aligned(16))) SrbdLds<W, NM> S;
   const int64_t i = blockIdx.x;
   if (i >= (a.count ? (int64_t)*a.count : a.batch)) return;
-#ifdef QLOCO_TRACE_SIMD  // development only (tools/simd_trace.py): placement + wall clock per instance
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-#endif
   srbd_solve_one<W, WS, NM, C2>(a, S, a.list ? (int64_t)a.list[i] : i);
-#ifdef QLOCO_TRACE_SIMD
-  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-  if (threadIdx.x == 0 && i < (1 << 18)) {
-    g_trace[4 * i + 0] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID
-    g_trace[4 * i + 1] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // XCC_ID[3:0]
-    g_trace[4 * i + 2] = (unsigned)t0;
-    g_trace[4 * i + 3] = (unsigned)t1;
-  }
-#endif
 }
 
 // Kernel classes by stance-leg count: 0 one wave (<= kW1Legs), 1..4 two
@@ -1539,82 +1391,127 @@ extern "C" void qloco_srbd_spec_default(qloco_srbd_spec *s) {
   s->polish = 0;
 }
 
-#ifdef QLOCO_TRACE_SIMD
-extern "C" int qloco_trace_read(unsigned int *host, size_t count) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace), count * sizeof(unsigned int), 0,
-                                  hipMemcpyDeviceToHost);
-}
-#endif
-#ifdef QLOCO_PHASE_TIMING
-extern "C" int qloco_phase_read(unsigned int *host, size_t count) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), count * sizeof(unsigned int), 0,
-                                  hipMemcpyDeviceToHost);
-}
-#endif
 
-// Scratch of the class dispatch: three instance lists of `cap` entries, their
-// counters, two side streams and the fork / join events -- one set per
-// (device, caller stream), so calls on different streams or threads never
-// share lists, counters or events (two calls on ONE stream are ordered by
-// it).  A captured HIP graph bakes the list pointers in, so a buffer is never
-// freed while the process lives: a larger batch allocates a new set and
-// retires the old one (kept, not freed -- no device-wide synchronisation on
-// the grow path either).  Growing inside a stream capture is refused
-// (QLOCO_ERR_ARG): run the largest batch once before capturing
-// (INTEGRATION.md).
+// Scratch of the class dispatch: the per-class instance lists (`cap` entries
+// each), their counters, three side streams and the fork / join events --
+// one set per (device, caller stream), so calls on different streams or
+// threads never share lists, counters or events (two calls on ONE stream
+// are ordered by it), and a capture on one stream never pulls another
+// caller's side streams into its graph.  The sets are bounded: at most
+// kScratchSets live ones, the least recently used beyond that is released
+// (its last class launch waited for by an event first), so callers that
+// spin up short-lived streams do not leak streams, events or memory.  A set
+// that ever served a stream capture is different: the graph baked its list
+// and counter pointers in, so its memory is pinned for the life of the
+// process (its streams and events are still released) -- as are the lists
+// it outgrew.  Growing inside a stream capture is refused (QLOCO_ERR_ARG):
+// run the largest batch once before capturing.  A captured
+// graph shares its set with later eager calls on the capture stream: replay
+// it ordered against them (graph capture).
 struct SrbdScratch {
   int *lists = nullptr;
   int *counts = nullptr;
   int64_t cap = 0;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
   hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t done = nullptr;  // recorded on the caller's stream after the last eager use
+  bool done_recorded = false;
+  bool captured = false;  // served a stream capture: memory pinned
+  uint64_t last_use = 0;
 };
+constexpr size_t kScratchSets = 8;
 static std::mutex g_srbd_scratch_mu;
 static std::map<std::pair<int, hipStream_t>, SrbdScratch> g_srbd_scratch;
-static std::vector<void *> g_srbd_retired;  // outgrown lists (a graph may still read them)
+static std::vector<void *> g_srbd_pinned;  // memory a captured graph may still read
+static uint64_t g_srbd_tick = 0;
+
+static void srbd_release(SrbdScratch &s) {
+  if (s.done_recorded) (void)hipEventSynchronize(s.done);
+  for (int k = 0; k < 3; ++k) {
+    if (s.side[k]) (void)hipStreamDestroy(s.side[k]);
+    if (s.join[k]) (void)hipEventDestroy(s.join[k]);
+  }
+  if (s.fork) (void)hipEventDestroy(s.fork);
+  if (s.done) (void)hipEventDestroy(s.done);
+  if (s.captured) {
+    g_srbd_pinned.push_back(s.lists);
+    g_srbd_pinned.push_back(s.counts);
+  } else {
+    if (s.lists) (void)hipFree(s.lists);
+    if (s.counts) (void)hipFree(s.counts);
+  }
+  s = SrbdScratch();
+}
+
+// Live scratch sets and pinned allocations (tests: the bound holds).
+extern "C" int qloco_srbd_scratch_sets(int32_t *pinned) {
+  std::lock_guard<std::mutex> lk(g_srbd_scratch_mu);
+  if (pinned) *pinned = (int32_t)g_srbd_pinned.size();
+  return (int)g_srbd_scratch.size();
+}
 
 // Caller holds g_srbd_scratch_mu for the whole enqueue sequence (counter
-// reset, classification, class launches): two threads sharing one stream
-// must not interleave their sequences on the shared counters.
-static int srbd_scratch(int64_t batch, hipStream_t st, SrbdScratch **out) {
+// reset, classification, class launches, the done event): two threads
+// sharing one stream must not interleave their sequences on the shared
+// counters.
+static int srbd_scratch(int64_t batch, hipStream_t st, bool capturing, SrbdScratch **out) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return QLOCO_ERR_DEVICE;
-  SrbdScratch &s = g_srbd_scratch[std::make_pair(dev, st)];
-  const bool fresh = !s.counts;
-  if (fresh || batch > s.cap) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+  const auto key = std::make_pair(dev, st);
+  auto it = g_srbd_scratch.find(key);
+  if (it == g_srbd_scratch.end()) {
+    if (capturing) {
       set_last_error("qloco_srbd_solve_ex: class-dispatch scratch must be sized before stream "
                      "capture (run the largest batch once on this stream first)",
                      hipErrorStreamCaptureUnsupported);
       return QLOCO_ERR_ARG;
     }
+    // bound the live sets: release the least recently used one first
+    if (g_srbd_scratch.size() >= kScratchSets) {
+      auto lru = g_srbd_scratch.begin();
+      for (auto j = g_srbd_scratch.begin(); j != g_srbd_scratch.end(); ++j)
+        if (j->second.last_use < lru->second.last_use) lru = j;
+      srbd_release(lru->second);
+      g_srbd_scratch.erase(lru);
+    }
+    it = g_srbd_scratch.emplace(key, SrbdScratch()).first;
   }
-  if (fresh) {
+  SrbdScratch &s = it->second;
+  if (!s.counts) {
     if (hipMalloc(&s.counts, 8 * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
     for (int k = 0; k < 3; ++k) {
       if (hipStreamCreateWithFlags(&s.side[k], hipStreamNonBlocking) != hipSuccess) return QLOCO_ERR_DEVICE;
       if (hipEventCreateWithFlags(&s.join[k], hipEventDisableTiming) != hipSuccess) return QLOCO_ERR_DEVICE;
     }
     if (hipEventCreateWithFlags(&s.fork, hipEventDisableTiming) != hipSuccess) return QLOCO_ERR_DEVICE;
+    if (hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return QLOCO_ERR_DEVICE;
   }
   if (batch > s.cap) {
+    if (capturing) {
+      set_last_error("qloco_srbd_solve_ex: class-dispatch scratch must be sized before stream "
+                     "capture (run the largest batch once on this stream first)",
+                     hipErrorStreamCaptureUnsupported);
+      return QLOCO_ERR_ARG;
+    }
     const int64_t cap = batch < 4096 ? 4096 : batch;
     int *lists = nullptr;
     if (hipMalloc(&lists, kSrbdClasses * cap * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
-    if (s.lists) g_srbd_retired.push_back(s.lists);
+    if (s.lists) {
+      if (s.captured) {
+        g_srbd_pinned.push_back(s.lists);  // a graph may still read the old lists
+      } else {
+        // every earlier use was enqueued on this stream
+        if (hipStreamSynchronize(st) != hipSuccess) return QLOCO_ERR_DEVICE;
+        (void)hipFree(s.lists);
+      }
+    }
     s.lists = lists;
     s.cap = cap;
   }
+  if (capturing) s.captured = true;
+  s.last_use = ++g_srbd_tick;
   *out = &s;
   return QLOCO_OK;
-}
-
-// Concurrent class launches (default) or all on the caller's stream
-// (QLOCO_SRBD_FORK=0, comparison runs).
-static bool srbd_fork_enabled() {
-  static const bool on = !(getenv("QLOCO_SRBD_FORK") && atoi(getenv("QLOCO_SRBD_FORK")) == 0);
-  return on;
 }
 
 extern "C" int qloco_srbd_max_stance_vars(void) { return 3 * kBigLegs; }
@@ -1696,42 +1593,35 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
   const dim3 grid((unsigned)batch);
   auto launch = [&](int cls, hipStream_t s) {
     if (cls == 0) {
-      if (a.N <= kShortN && kShortWpe > 0) {
+      if (a.N <= kShortN) {
         // short horizons: per-step tables sized for N <= 10 (9 KB of LDS) so
         // 16 one-wave workgroups share a CU -- four waves per SIMD
         if (ws)
-          hipLaunchKernelGGL((srbd_admm_kernel<1, (kShortWpe > 0 ? kShortWpe : 1), true, kShortN>), grid, dim3(64), 0, s, a);
+          hipLaunchKernelGGL((srbd_admm_kernel<1, kShortWpe, true, kShortN>), grid, dim3(64), 0, s, a);
         else
-          hipLaunchKernelGGL((srbd_admm_kernel<1, (kShortWpe > 0 ? kShortWpe : 1), false, kShortN>), grid, dim3(64), 0, s, a);
+          hipLaunchKernelGGL((srbd_admm_kernel<1, kShortWpe, false, kShortN>), grid, dim3(64), 0, s, a);
       } else if (batch <= kSmallBatch) {
         if (ws)
-          hipLaunchKernelGGL((srbd_admm_kernel<1, 2, true>), grid, dim3(64), 0, s, a);
+          hipLaunchKernelGGL((srbd_admm_kernel<1, kW1SmallWpe, true>), grid, dim3(64), 0, s, a);
         else
-          hipLaunchKernelGGL((srbd_admm_kernel<1, 2, false>), grid, dim3(64), 0, s, a);
+          hipLaunchKernelGGL((srbd_admm_kernel<1, kW1SmallWpe, false>), grid, dim3(64), 0, s, a);
       } else {
         if (ws)
-          hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, true>), grid, dim3(64), 0, s, a);
+          hipLaunchKernelGGL((srbd_admm_kernel<1, kW1Wpe, true>), grid, dim3(64), 0, s, a);
         else
-          hipLaunchKernelGGL((srbd_admm_kernel<1, QLOCO_SRBD_WAVES_PER_EU, false>), grid, dim3(64), 0, s, a);
+          hipLaunchKernelGGL((srbd_admm_kernel<1, kW1Wpe, false>), grid, dim3(64), 0, s, a);
       }
     } else if (cls <= 4) {  // two-wave column buckets C2 = 3 / 6 / 9 / 15
-      constexpr int WP = QLOCO_SRBD_WAVES_PER_EU_W2;
       if (ws)  // srbd_class_of routes every warm two-wave instance to bucket 4
-        hipLaunchKernelGGL((srbd_admm_kernel<2, WP, true, kMaxN, 15>), grid, dim3(128), 0, s, a);
-      // the narrow buckets fit 168 VGPRs: three waves per SIMD
-      else if (cls == 1 && a.N <= kShortN && kW2ShortWpe > 0)
-        // N <= 10: per-step LDS tables for N <= 10 (17 KB per workgroup)
-        hipLaunchKernelGGL((srbd_admm_kernel<2, (kW2ShortWpe > 0 ? kW2ShortWpe : 1), false, kShortN, 3>), grid, dim3(128), 0, s, a);
+        hipLaunchKernelGGL((srbd_admm_kernel<2, kW2WarmWpe, true, kMaxN, 15>), grid, dim3(128), 0, s, a);
       else if (cls == 1)
-        hipLaunchKernelGGL((srbd_admm_kernel<2, 3, false, kMaxN, 3>), grid, dim3(128), 0, s, a);
-      else if (cls == 2 && a.N <= kShortN && kW2C6ShortWpe > 0)
-        hipLaunchKernelGGL((srbd_admm_kernel<2, (kW2C6ShortWpe > 0 ? kW2C6ShortWpe : 1), false, kShortN, 6>), grid, dim3(128), 0, s, a);
+        hipLaunchKernelGGL((srbd_admm_kernel<2, kW2Wpe, false, kMaxN, 3>), grid, dim3(128), 0, s, a);
       else if (cls == 2)
-        hipLaunchKernelGGL((srbd_admm_kernel<2, 3, false, kMaxN, 6>), grid, dim3(128), 0, s, a);
+        hipLaunchKernelGGL((srbd_admm_kernel<2, kW2Wpe, false, kMaxN, 6>), grid, dim3(128), 0, s, a);
       else if (cls == 3)
-        hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_W2_C9_WPE, false, kMaxN, 9>), grid, dim3(128), 0, s, a);
+        hipLaunchKernelGGL((srbd_admm_kernel<2, kW2Wpe, false, kMaxN, 9>), grid, dim3(128), 0, s, a);
       else
-        hipLaunchKernelGGL((srbd_admm_kernel<2, QLOCO_SRBD_W2_C15_WPE, false, kMaxN, 15>), grid, dim3(128), 0, s, a);
+        hipLaunchKernelGGL((srbd_admm_kernel<2, kW2Wpe, false, kMaxN, 15>), grid, dim3(128), 0, s, a);
     } else {  // wide kernel half widths HC = 96 / 112 / 120
       if (ws)  // srbd_class_of routes every warm wide instance to class 7: one
                // warm instantiation at the full 128-column halves
@@ -1751,14 +1641,17 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
     launch(top, st);
   } else {
     std::lock_guard<std::mutex> lk(g_srbd_scratch_mu);
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    const bool capturing =
+        hipStreamIsCapturing(st, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone;
     SrbdScratch *sc = nullptr;
-    const int rc = srbd_scratch(batch, st, &sc);
+    const int rc = srbd_scratch(batch, st, capturing, &sc);
     if (rc != QLOCO_OK) return rc;
     QLOCO_HIP_CHECK(hipMemsetAsync(sc->counts, 0, 8 * sizeof(int), st), "class counters");
     hipLaunchKernelGGL(srbd_classify_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st,
                        a, top, sc->lists, sc->cap, sc->counts);
     QLOCO_HIP_CHECK(hipGetLastError(), "srbd_classify_kernel launch");
-    const bool fork = srbd_fork_enabled();
+    const bool fork = true;  // classes on the side streams (concurrent tails)
     if (fork) QLOCO_HIP_CHECK(hipEventRecord(sc->fork, st), "fork event");
     // class 0 on the caller's stream; two-wave buckets 1 / 3 on side stream
     // 0 and 2 / 4 on side stream 1 (a bucket's tail overlaps the next one's
@@ -1790,6 +1683,11 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
         QLOCO_HIP_CHECK(hipEventRecord(sc->join[sd], s), "join event");
         QLOCO_HIP_CHECK(hipStreamWaitEvent(st, sc->join[sd], 0), "join wait");
       }
+    }
+    // the set's last eager use (what a later release waits for)
+    if (!capturing) {
+      QLOCO_HIP_CHECK(hipEventRecord(sc->done, st), "scratch done event");
+      sc->done_recorded = true;
     }
   }
   QLOCO_HIP_CHECK(hipGetLastError(), "srbd_admm_kernel launch");

@@ -129,10 +129,14 @@ def test_argument_validation_without_device_work():
     assert L.qloco_srbd_solve(C.byref(sp), 4, *([None] * 10), None) == 100
     # EiQuadProg limits: QPBaseClass's capacity (nVars <= 60, nIneq <= 300,
     # QPBaseClass.h:49-51) rounded up -- n, p <= 64, m <= 320
-    assert L.qloco_max_gi_vars() == 64
     lim = (C.c_int32 * 3)()
     L.qloco_gi_limits(C.byref(lim, 0), C.byref(lim, 4), C.byref(lim, 8))
     assert list(lim) == [64, 64, 320]
+    # the fast path (four QPs per wavefront): qloco_max_gi_vars keeps its
+    # round-1 meaning, qloco_gi_fast_limits gives all three
+    assert L.qloco_max_gi_vars() == 16
+    L.qloco_gi_fast_limits(C.byref(lim, 0), C.byref(lim, 4), C.byref(lim, 8))
+    assert list(lim) == [16, 16, 64]
     args = [None, 0] * 6 + [None] * 4 + [None]
     assert L.qloco_eiquadprog_solve(65, 0, 8, 1, *args) == 4
     assert L.qloco_eiquadprog_solve(8, 65, 8, 1, *args) == 4

@@ -31,7 +31,8 @@ pytestmark = pytest.mark.gpu
 import oracle_lib as O  # noqa: E402
 from srbd_ref import Instance, np_build  # noqa: E402
 
-from quadrupedal_loco_amd import srbd  # noqa: E402
+from quadrupedal_loco_amd import _lib, srbd  # noqa: E402
+import ctypes as C  # noqa: E402
 
 SEED = 20261015
 
@@ -801,3 +802,38 @@ def test_srbd_graph_capture_replay():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out.u, ref.u)
+
+
+def test_srbd_scratch_bounded_over_short_lived_streams():
+    """A caller that makes a new stream per call: the class-dispatch
+    scratch stays bounded -- at most 8 live sets, the least recently used one
+    released once its last launch is done -- and every call still gives the
+    default stream's results bit for bit.  The set of the captured stream of
+    test_srbd_graph_capture_replay (same process) may be pinned, never freed."""
+    dev = _dev()
+    N = 20
+    a = _three_class_batch(N)
+    ta = [torch.from_numpy(np.ascontiguousarray(v)).to(dev) for v in a]
+    solver = srbd.BatchedConvexMpc(horizon=N)
+    ref = solver.solve(*ta, full=True)
+    torch.cuda.synchronize()
+    L = _lib.lib()
+    pinned = C.c_int32(0)
+    for k in range(24):
+        s = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            o = solver.solve(*ta, full=True, stream=s.cuda_stream)
+        s.synchronize()
+        assert torch.equal(o.u, ref.u) and torch.equal(o.iters, ref.iters)
+        del s
+        live = L.qloco_srbd_scratch_sets(C.byref(pinned))
+        assert live <= 8, (k, live)
+    assert L.qloco_srbd_scratch_sets(None) == 8
+    before = pinned.value
+    for k in range(8):  # more churn: nothing new gets pinned by eager calls
+        s = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            solver.solve(*ta, full=True, stream=s.cuda_stream)
+        s.synchronize()
+    L.qloco_srbd_scratch_sets(C.byref(pinned))
+    assert pinned.value == before
