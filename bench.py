@@ -192,6 +192,9 @@ def main():
                     help="N > 1: run each step's all-gather under the next solve (double-"
                          "buffered u0); off by default: on one GPU the RCCL kernel sharing "
                          "the CUs with the solve cost more than it hid (DESIGN.md §7)")
+    ap.add_argument("--comm", choices=("torch", "capi"), default="torch",
+                    help="N > 1: who shards and all-gathers -- torch.distributed (dist.py) or the "
+                         "library's own C-ABI handles (qloco_mgpu_*: RCCL from C, include/qloco.h 10)")
     ap.add_argument("--force-dist", action="store_true",
                     help="testing: run the N > 1 code path (RCCL group, all-gather) at N = 1")
     ap.add_argument("--dist-selftest", action="store_true",
@@ -240,6 +243,14 @@ def main():
         first, stride, _ = interleaved_shard(B, world, rank)
     else:
         (first, _), stride = shard_range(B, rank), 1
+    multi = world > 1 or args.force_dist
+    capi = multi and args.comm == "capi" and not args.no_allgather
+    if capi:
+        # the C handles own the shard arithmetic: take this rank's ids from them
+        from quadrupedal_loco_amd import mgpu
+        mode = mgpu.INTERLEAVED if shard == "interleaved" else mgpu.CONTIGUOUS
+        first, count, stride = mgpu.shard(B * world, world, rank, mode)
+        assert count == B
     x0, xr, ft, ct = srbd.generate(SEED, N, B, args.gait, first=first, stride=stride)
     d_x0 = torch.from_numpy(x0).to(dev)
     d_xr = torch.from_numpy(xr).to(dev)
@@ -248,9 +259,13 @@ def main():
     solver = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=int(args.literal))
     legs = 4 * N if args.literal else srbd.max_stance_legs(ct, N)
     gather = None
-    multi = world > 1 or args.force_dist
-    overlap = multi and not args.no_allgather and args.overlap
-    if multi and not args.no_allgather:
+    overlap = multi and not args.no_allgather and args.overlap and not capi
+    handle = None
+    if capi:
+        cid = [mgpu.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(cid, src=0)
+        handle = mgpu.MgpuSolver(solver.spec, B * world, world, rank, cid[0], mode)
+    elif multi and not args.no_allgather:
         from quadrupedal_loco_amd.dist import ForceGather
         gather = [ForceGather(B, device=dev) for _ in range(2 if overlap else 1)]
     # two output sets when the all-gather of step i overlaps the solve of step
@@ -267,6 +282,10 @@ def main():
             pending[i % 2] = None
         if ev is not None:
             ev[0].record(stream)
+        if handle is not None:  # solve + all-gather + global order, all in the C library
+            handle.solve(d_x0, d_xr, d_ft, d_ct, max_legs=legs,
+                         stream=stream.cuda_stream)
+            return
         solver.solve(d_x0, d_xr, d_ft, d_ct, out=o, max_legs=legs, stream=stream.cuda_stream)
         if ev is not None and ev[1] is not None:
             ev[1].record(stream)
@@ -324,6 +343,9 @@ def main():
         gather_ms = np.zeros(K)
 
     # per-instance stats of the solved batch (identical every step)
+    if handle is not None:  # stats not gathered in the timed loop: one plain solve
+        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, max_legs=legs, stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
     status = out.status.cpu().numpy()
     iters = out.iters.cpu().numpy()
     rho_up = out.rho_updates.cpu().numpy()
@@ -355,8 +377,9 @@ def main():
             "solver": "OSQP-algorithm ADMM, default settings (eps 1e-3, adaptive rho), %s" % (
                 "literal 12N-variable QP (literal_full_qp=1)" if args.literal else
                 "stance-only reduction of the 12N-variable QP (same optimum)"),
-            "parallelism": "dp%d (%s instance shards, RCCL all-gather of u0%s)" % (
-                world, shard, ", overlapped with the next solve" if overlap else ""),
+            "parallelism": "dp%d (%s instance shards, RCCL all-gather of u0%s%s)" % (
+                world, shard, ", overlapped with the next solve" if overlap else "",
+                ", C-ABI handles qloco_mgpu_*" if capi else ""),
         },
         "p99_batch_us": round(float(np.percentile(step_ms, 99)) * 1e3, 2),
         "p50_batch_us": round(float(np.percentile(step_ms, 50)) * 1e3, 2),
@@ -397,6 +420,8 @@ def main():
         res["cpu_baseline"] = cpu_baseline(N, args.gait, args.cpu_seconds, args.cpu_threads)
     if rank == 0:
         print(json.dumps(res), file=json_out, flush=True)
+    if handle is not None:
+        handle.close()
     if dist is not None:
         dist.destroy_process_group()
 

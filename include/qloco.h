@@ -421,6 +421,54 @@ int qloco_a1_qp_solve(const qloco_a1_params *prm, int64_t batch, const double *s
                       int32_t *status, int32_t *iters, int32_t *rho_updates, double *obj,
                       void *stream);
 
+/* ====================================================================== */
+/* 10. Multi-GPU handles                         */
+/*    The instances are independent: each rank (one process or thread per */
+/*    GPU) solves its own shard of the global batch with                   */
+/*    qloco_srbd_solve_ex and ONE RCCL all-gather over xGMI, on the        */
+/*    caller's stream, leaves every rank with u0 of the whole batch in     */
+/*    global instance order.  Replaces nothing in the reference (its       */
+/*    controllers are one process each, A1RobotControl.cpp:553-578); it is */
+/*    the C++ caller's way to shard.  RCCL (librccl.so.1) is loaded on     */
+/*    first use.                                                           */
+/* ====================================================================== */
+#define QLOCO_MGPU_ID_BYTES 128
+enum {
+  QLOCO_SHARD_CONTIGUOUS = 0,  /* balanced contiguous ranges                        */
+  QLOCO_SHARD_INTERLEAVED = 1  /* ids rank, rank + world, ... (divergent schedules) */
+};
+typedef struct qloco_mgpu qloco_mgpu;
+/* Global ids owned by `rank`: first + k * stride, k < count.  Contiguous:
+ * first = rank * (total / world) + min(rank, total % world), count = total /
+ * world (+1 for rank < total % world), stride 1.  Interleaved: first = rank,
+ * stride = world, count = ceil((total - rank) / world).  Host only. */
+int qloco_mgpu_shard(int64_t total, int32_t world, int32_t rank, int32_t mode, int64_t *first,
+                     int64_t *count, int64_t *stride);
+/* Row of global id g in the gathered (world x P) buffer, P = ceil(total /
+ * world) the padded shard: rows[g] = owner * P + position.  Host only (the
+ * device reorder uses the same map). */
+int qloco_mgpu_gather_rows(int64_t total, int32_t world, int32_t mode, int64_t *rows);
+/* Rank 0: a new communicator id; the caller ships the bytes to every rank. */
+int qloco_mgpu_unique_id(uint8_t *id /* [QLOCO_MGPU_ID_BYTES] */);
+/* Collective: every rank, with its device current, the same id / world /
+ * total / mode.  Allocates the rank's padded shard buffers on that device. */
+int qloco_mgpu_init(qloco_mgpu **h, const uint8_t *id, int32_t world, int32_t rank, int64_t total,
+                    int32_t mode);
+/* This rank's shard (first, count, stride) and the padded shard size P. */
+int qloco_mgpu_info(const qloco_mgpu *h, int64_t *first, int64_t *count, int64_t *stride,
+                    int64_t *padded);
+/* Solve this rank's shard -- x0 / x_ref / feet / contacts / warm hold ITS
+ * `count` instances, laid out as for qloco_srbd_solve_ex -- then all-gather:
+ * u0_all[total*12] (required), status_all[total], iters_all[total]
+ * (optional) in global id order on every rank.  Collective and stream-
+ * ordered on `stream` (the handle's device must be current). */
+int qloco_mgpu_solve(qloco_mgpu *h, const qloco_srbd_spec *spec, const float *x0,
+                     const float *x_ref, const float *feet, const uint8_t *contacts, float *warm,
+                     float *u0_all, int32_t *status_all, int32_t *iters_all,
+                     int32_t max_stance_legs, void *stream);
+/* Releases the communicator and the buffers (NULL is a no-op). */
+int qloco_mgpu_destroy(qloco_mgpu *h);
+
 #ifdef __cplusplus
 }
 #endif

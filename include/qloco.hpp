@@ -207,6 +207,21 @@ struct A1MpcState {                // the A1CtrlStates fields compute_grf reads
 class ConvexMpcBatch {
  public:
   ConvexMpcBatch(int batch, const qloco_srbd_spec *spec = nullptr);
+  // Multi-GPU (include/qloco.h §10): this object is rank `rank` of `world`
+  // (one process or thread per GPU, its device current) over a global batch
+  // of `total` robots.  It owns the shard qloco_mgpu_shard assigns
+  // (shard_first + k * shard_stride, k < shard_count): compute_grf takes and
+  // returns that shard, and one RCCL all-gather per call leaves every
+  // robot's forces (same frame, same NaN guard) in all_forces(), total * 12,
+  // on every rank.  comm_id: qloco_mgpu_unique_id() on rank 0, shipped to
+  // the other ranks by the caller (QLOCO_MGPU_ID_BYTES bytes).
+  ConvexMpcBatch(int64_t total, int world, int rank, const uint8_t *comm_id,
+                 int shard_mode = QLOCO_SHARD_CONTIGUOUS, const qloco_srbd_spec *spec = nullptr);
+  ~ConvexMpcBatch();
+  ConvexMpcBatch(const ConvexMpcBatch &) = delete;
+  ConvexMpcBatch &operator=(const ConvexMpcBatch &) = delete;
+  const std::vector<double> &all_forces() const { return all_forces_; }
+  int64_t shard_first = 0, shard_count = 0, shard_stride = 1;
   // foot_forces_grf: B * 12 (3x4 col-major per robot), in/out
   void compute_grf(const A1MpcState *states, double *foot_forces_grf);
   // device-resident form (inputs already in HBM): thin wrapper of qloco_srbd_solve_ex
@@ -227,6 +242,12 @@ class ConvexMpcBatch {
   float *d_x0_, *d_xr_, *d_feet_, *d_u0_, *d_rec_ = nullptr;
   uint8_t *d_ct_;
   int32_t *d_st_, *d_it_;
+  // multi-GPU form
+  qloco_mgpu *mg_ = nullptr;
+  int64_t total_ = 0;
+  float *d_u0_all_ = nullptr;
+  int32_t *d_st_all_ = nullptr, *d_it_all_ = nullptr;
+  std::vector<double> all_forces_;
 };
 
 // ------------------------------------------------------------------------

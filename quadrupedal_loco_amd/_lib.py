@@ -95,6 +95,13 @@ SIGNATURES = {
     "qloco_support_phase": (C.c_int, [i64] + [vp] * 8),
     "qloco_a1_params_default": (None, [C.POINTER(A1Params)]),
     "qloco_a1_qp_solve": (C.c_int, [C.POINTER(A1Params), i64] + [vp] * 9),
+    "qloco_mgpu_shard": (C.c_int, [i64, i32, i32, i32, vp, vp, vp]),
+    "qloco_mgpu_gather_rows": (C.c_int, [i64, i32, i32, vp]),
+    "qloco_mgpu_unique_id": (C.c_int, [vp]),
+    "qloco_mgpu_init": (C.c_int, [vp, vp, i32, i32, i64, i32]),
+    "qloco_mgpu_info": (C.c_int, [vp, vp, vp, vp, vp]),
+    "qloco_mgpu_solve": (C.c_int, [vp, C.POINTER(SrbdSpec), vp, vp, vp, vp, vp, vp, vp, vp, i32, vp]),
+    "qloco_mgpu_destroy": (C.c_int, [vp]),
 }
 
 

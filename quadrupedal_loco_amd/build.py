@@ -30,6 +30,7 @@ SOURCES = [
     "qloco_rt.hip",
     "qloco_servo.hip",
     "qloco_a1qp.hip",
+    "qloco_mgpu.hip",
     "qloco_gen.cpp",
 ]
 # per-file extra flags: the fp64 active-set kernel keeps the restatement's
@@ -83,7 +84,7 @@ def build(verbose=False, jobs=8):
             sys.stderr.write(out.decode())
             raise RuntimeError("hipcc failed: " + " ".join(cmd))
     if cmds or not os.path.exists(LIB) or _needs(LIB, objs):
-        link = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        link = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-ldl"]
         if verbose:
             print(" ".join(link))
         subprocess.run(link, check=True)

@@ -8,6 +8,9 @@ static thread_local char g_last_error[256] = {0};
 void set_last_error(const char *where, hipError_t e) {
   snprintf(g_last_error, sizeof(g_last_error), "%s: %s", where, hipGetErrorString(e));
 }
+void set_last_error_msg(const char *where, const char *what) {
+  snprintf(g_last_error, sizeof(g_last_error), "%s: %s", where, what);
+}
 }  // namespace qloco
 
 extern "C" const char *qloco_last_error(void) { return qloco::g_last_error; }

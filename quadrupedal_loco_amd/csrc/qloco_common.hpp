@@ -11,6 +11,8 @@ namespace qloco {
 
 // thread-local last HIP error (qloco_last_error)
 void set_last_error(const char *where, hipError_t e);
+// the same with a library message instead of a HIP error (RCCL, dlopen)
+void set_last_error_msg(const char *where, const char *what);
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdint>
 #include <cstring>
 
 namespace qloco {
@@ -410,6 +411,32 @@ ConvexMpcBatch::ConvexMpcBatch(int batch, const qloco_srbd_spec *sp)
   iters.assign(B, 0);
 }
 
+static int shard_count_of(int64_t total, int world, int rank, int mode) {
+  int64_t count = 0;
+  if (qloco_mgpu_shard(total, world, rank, mode, nullptr, &count, nullptr) != QLOCO_OK)
+    throw Error("ConvexMpcBatch: invalid shard (total, world, rank, mode)", QLOCO_ERR_ARG);
+  if (count < 1 || count > INT32_MAX)
+    throw Error("ConvexMpcBatch: this rank's shard is empty or too large", QLOCO_BAD_SIZE);
+  return (int)count;
+}
+
+ConvexMpcBatch::ConvexMpcBatch(int64_t total, int world, int rank, const uint8_t *comm_id,
+                               int shard_mode, const qloco_srbd_spec *sp)
+    : ConvexMpcBatch(shard_count_of(total, world, rank, shard_mode), sp) {
+  abi_ok(qloco_mgpu_shard(total, world, rank, shard_mode, &shard_first, &shard_count, &shard_stride),
+         "qloco_mgpu_shard");
+  total_ = total;
+  d_u0_all_ = dalloc<float>(arena_, (size_t)total * 12);
+  d_st_all_ = dalloc<int32_t>(arena_, (size_t)total);
+  d_it_all_ = dalloc<int32_t>(arena_, (size_t)total);
+  all_forces_.assign((size_t)total * 12, 0.0);
+  abi_ok(qloco_mgpu_init(&mg_, comm_id, world, rank, total, shard_mode), "qloco_mgpu_init");
+}
+
+ConvexMpcBatch::~ConvexMpcBatch() {
+  if (mg_) qloco_mgpu_destroy(mg_);
+}
+
 void ConvexMpcBatch::check_spec() const {
   if (spec.horizon != horizon_)
     throw Error("ConvexMpcBatch: spec.horizon changed after construction (buffers sized for " +
@@ -429,6 +456,9 @@ void ConvexMpcBatch::reset() {
 void ConvexMpcBatch::solve_device(const float *x0, const float *x_ref, const float *feet,
                                   const uint8_t *contacts, float *u0, int32_t *st, int32_t *it) {
   check_spec();
+  if (mg_)
+    throw Error("ConvexMpcBatch::solve_device: a multi-GPU object solves through compute_grf "
+                "(or qloco_mgpu_solve directly)", QLOCO_ERR_ARG);
   const int32_t legs = 4 * horizon_;  // constant contacts over the horizon: 4N worst case
   abi_ok(qloco_srbd_solve_ex(&spec, batch_, x0, x_ref, feet, contacts, u0, nullptr, st, it,
                              nullptr, nullptr, d_rec_, legs, arena_.stream()),
@@ -488,6 +518,35 @@ void ConvexMpcBatch::compute_grf(const A1MpcState *s, double *forces) {
   arena_.upload(d_xr_, xr.data(), sizeof(float) * B * 13 * N);
   arena_.upload(d_feet_, feet.data(), sizeof(float) * B * 12);
   arena_.upload(d_ct_, ct.data(), B * 4);
+  if (mg_) {  // this rank's shard, then one all-gather of every robot's u0
+    abi_ok(qloco_mgpu_solve(mg_, &spec, d_x0_, d_xr_, d_feet_, d_ct_, d_rec_, d_u0_all_, d_st_all_,
+                            d_it_all_, maxlegs, arena_.stream()),
+           "qloco_mgpu_solve");
+    const size_t T = (size_t)total_;
+    std::vector<float> ua(T * 12);
+    std::vector<int32_t> sa(T), ia(T);
+    arena_.download(ua.data(), d_u0_all_, sizeof(float) * T * 12);
+    arena_.download(sa.data(), d_st_all_, sizeof(int32_t) * T);
+    arena_.download(ia.data(), d_it_all_, sizeof(int32_t) * T);
+    arena_.sync();
+    for (size_t g = 0; g < T; ++g)
+      for (int l = 0; l < 4; ++l) {
+        const float *f = &ua[g * 12 + 3 * l];
+        if (std::isnan(f[0]) || std::isnan(f[1]) || std::isnan(f[2])) continue;  // :597 guard
+        for (int c = 0; c < 3; ++c) all_forces_[g * 12 + 3 * l + c] = f[c];
+      }
+    for (size_t b = 0; b < B; ++b) {
+      const size_t g = (size_t)(shard_first + (int64_t)b * shard_stride);
+      status[b] = sa[g];
+      iters[b] = ia[g];
+      for (int l = 0; l < 4; ++l) {
+        const float *f = &ua[g * 12 + 3 * l];
+        if (std::isnan(f[0]) || std::isnan(f[1]) || std::isnan(f[2])) continue;
+        for (int c = 0; c < 3; ++c) forces[b * 12 + 3 * l + c] = f[c];
+      }
+    }
+    return;
+  }
   abi_ok(qloco_srbd_solve_ex(&spec, batch_, d_x0_, d_xr_, d_feet_, d_ct_, d_u0_, nullptr, d_st_,
                              d_it_, nullptr, nullptr, d_rec_, maxlegs, arena_.stream()),
          "qloco_srbd_solve_ex");

@@ -268,6 +268,49 @@ static void test_convex_mpc_persistent() {
   std::printf("persistent compute_grf ok: cold %d iters, resumed %d\n", cold, mpc.iters[1]);
 }
 
+// The multi-GPU form at world 1 (RCCL with one rank): a ConvexMpcBatch over
+// a global batch of 5 robots, interleaved shard mode, gives the single-GPU
+// object's forces, status and iterations exactly, in all_forces() and in its
+// own shard's outputs.
+static void test_convex_mpc_multi_gpu() {
+  const int T = 5;
+  std::vector<qloco::A1MpcState> st(T);
+  for (int b = 0; b < T; ++b) {
+    auto &s = st[b];
+    s.root_pos[2] = 0.30;
+    s.root_pos_d[2] = 0.30;
+    s.root_euler[2] = 0.1 * b;
+    s.root_lin_vel[0] = 0.05 * b;
+    const double c = std::cos(0.1 * b), sn = std::sin(0.1 * b);
+    const double R[9] = {c, sn, 0, -sn, c, 0, 0, 0, 1};
+    for (int k = 0; k < 9; ++k) s.root_rot_mat[k] = R[k];
+    const double feet[12] = {0.15, 0.127, -0.31, 0.15, -0.127, -0.31,
+                             -0.225, 0.127, -0.31, -0.225, -0.127, -0.31};
+    for (int k = 0; k < 12; ++k) s.foot_pos_abs[k] = feet[k];
+    const bool ph = b & 1;
+    s.contacts[0] = s.contacts[3] = ph;
+    s.contacts[1] = s.contacts[2] = !ph;
+  }
+  qloco::ConvexMpcBatch one(T);
+  std::vector<double> f1(T * 12, 0.0), f2(T * 12, 0.0);
+  one.compute_grf(st.data(), f1.data());
+  uint8_t id[QLOCO_MGPU_ID_BYTES];
+  CHECK(qloco_mgpu_unique_id(id) == QLOCO_OK, "qloco_mgpu_unique_id: %s", qloco_last_error());
+  qloco::ConvexMpcBatch mg(T, 1, 0, id, QLOCO_SHARD_INTERLEAVED);
+  CHECK(mg.shard_first == 0 && mg.shard_count == T && mg.shard_stride == 1, "world-1 shard");
+  for (int call = 0; call < 2; ++call) {  // the persistent update path too
+    if (call == 1) one.compute_grf(st.data(), f1.data());
+    mg.compute_grf(st.data(), f2.data());
+    for (int k = 0; k < T * 12; ++k) {
+      CHECK(f2[k] == f1[k], "call %d: shard forces [%d] %.6f vs %.6f", call, k, f2[k], f1[k]);
+      CHECK(mg.all_forces()[k] == f1[k], "call %d: all_forces [%d]", call, k);
+    }
+    for (int b = 0; b < T; ++b)
+      CHECK(mg.status[b] == one.status[b] && mg.iters[b] == one.iters[b], "call %d: stats %d", call, b);
+  }
+  std::printf("multi-GPU compute_grf ok (world 1): iters %d / %d\n", mg.iters[0], mg.iters[1]);
+}
+
 // A1RobotControl::compute_grf QP branch (A1QpBatch) vs oracle/a1_qp.c.
 static void test_a1_qp() {
   const int B = 8;
@@ -496,6 +539,7 @@ int main() {
     test_body_mpc();
     test_convex_mpc();
     test_convex_mpc_persistent();
+    test_convex_mpc_multi_gpu();
     test_a1_qp();
     test_kinematics();
     test_rt_node();

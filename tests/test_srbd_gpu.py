@@ -358,6 +358,49 @@ def test_srbd_vs_literal_full_qp_restatement(N, B, gait):
     assert same >= 0.6 * B, same
 
 
+def test_srbd_two_wave_c6_bucket_regression():
+    """Round-3 divergence regression: the
+    26-29-leg instances of mixed N = 10 schedules run in the C2 = 6 two-wave
+    bucket.  48 such instances against the fp64 restatement (status,
+    iterations within one check and equal for >= 90 %, u0 / objective bounds
+    of test_srbd_matches_admm_restatement), then the same 48 replicated to
+    6,144 instances in one launch -- every SIMD holding several of them, so
+    the two waves' LDS hand-offs run under full load -- must give each
+    replica bit-identical results."""
+    dev = _dev()
+    N = 10
+    x0, xr, ft, ct = srbd.generate(SEED, N, 4096, "mixed")
+    legs = ct.reshape(len(ct), -1).astype(bool).sum(axis=1)
+    pick = np.nonzero((legs >= 26) & (legs <= 29))[0][:48]
+    assert len(pick) == 48 and set(np.unique(legs[pick])) >= {26, 28}
+    a = [np.ascontiguousarray(v[pick]) for v in (x0, xr, ft, ct)]
+    solver = srbd.BatchedConvexMpc(horizon=N)
+    out = solver.solve(*(torch.from_numpy(v).to(dev) for v in a), full=True)
+    torch.cuda.synchronize()
+    u = out.u.cpu().numpy().astype(np.float64)
+    st, it = out.status.cpu().numpy(), out.iters.cpu().numpy()
+    sp = O.srbd_spec(N=N)
+    same = 0
+    for b in range(len(pick)):
+        inst = Instance(sp, a[0][b], a[1][b], a[2][b], a[3][b])
+        xref, info = inst.admm_reduced()
+        assert st[b] == 0 and info.status == 0, (b, st[b], info.status)
+        assert abs(int(it[b]) - info.iters) <= 25, (b, it[b], info.iters)
+        same += int(it[b]) == info.iters
+        assert np.abs(u[b, :12] - xref[:12]).max() <= 5.0, b
+        fr = inst.obj(xref)
+        assert abs(inst.obj(u[b]) - fr) <= 1e-3 * max(1.0, abs(fr)), b
+    assert same >= 0.9 * len(pick), same
+    R = 128
+    big = [torch.from_numpy(np.ascontiguousarray(np.tile(v, (R, 1)))).to(dev) for v in a]
+    ob = solver.solve(*big, full=True)
+    torch.cuda.synchronize()
+    ub = ob.u.cpu().numpy().reshape(R, len(pick), -1)
+    ib = ob.iters.cpu().numpy().reshape(R, len(pick))
+    assert np.array_equal(ib, np.tile(it, (R, 1)))
+    assert np.array_equal(ub, np.tile(out.u.cpu().numpy(), (R, 1, 1)))
+
+
 def test_srbd_config4_share_sampled_against_oracle():
     """BASELINE configs[3] per-GPU share at full size: Go1 pace N = 20,
     65,536 instances in one launch.  Whole batch: every instance converges,
@@ -638,6 +681,46 @@ def test_srbd_literal_matches_full_restatement(N, B, gait):
         assert np.array_equal(r["u0"][b], r["u"][b][:12])
     assert same >= 0.9 * B, same
     assert near >= (0.9 if N <= 10 else 0.85) * B, near
+
+
+@pytest.mark.parametrize("N,B,gait,samples", [(10, 4096, "trot", 16), (16, 65536, "trot", 8),
+                                              (20, 65536, "pace", 6)])
+def test_srbd_literal_full_size_sampled(N, B, gait, samples):
+    """The literal QP at full size, one launch each: BASELINE configs[1]
+    (N = 10 trot, 4096) and the per-GPU shares of configs[2] / [3] (N = 16
+    trot, N = 20 pace: 65,536 each; the wide 512-thread kernel).  Whole
+    batch: every instance converges, forces finite and inside the friction
+    pyramid, swing forces within the ADMM tolerance of zero, u0 = u[:12], and
+    a second launch is bit-identical.  Instances spread over the batch (both
+    ends, both phases) against the fp64 restatement of the same 12N-variable
+    OSQP call (Instance.admm_full) at test_srbd_literal_matches_full_
+    restatement's per-instance bounds."""
+    (x0, xr, ft, ct), r = _solve(N, B, gait, literal_full_qp=1)
+    assert np.all(r["status"] == 0), np.unique(r["status"], return_counts=True)
+    u = r["u"].reshape(B, N, 4, 3)
+    assert np.all(np.isfinite(u))
+    tol = 0.25
+    assert np.all(u[..., 2] >= -tol) and np.all(u[..., 2] <= 180 + tol)
+    assert np.all(np.abs(u[..., 0]) <= 0.3 * u[..., 2] + tol)
+    assert np.all(np.abs(u[..., 1]) <= 0.3 * u[..., 2] + tol)
+    swing = ct.reshape(B, N, 4) == 0
+    assert np.abs(u[swing]).max() <= tol
+    assert np.array_equal(r["u0"], r["u"][:, :12])
+    _, r2 = _solve(N, B, gait, literal_full_qp=1)
+    assert np.array_equal(r["u"], r2["u"]) and np.array_equal(r["iters"], r2["iters"])
+    sp = O.srbd_spec(N=N)
+    for b in np.linspace(0, B - 1, samples).astype(int):
+        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
+        xf, info = inst.admm_full()
+        assert info.status == 0
+        assert abs(int(r["iters"][b]) - info.iters) <= 25, (b, r["iters"][b], info.iters)
+        ub = r["u"][b].astype(np.float64)
+        du0, dF, dM, dX = _traj_metrics(ub, xf, x0[b], xr[b], ft[b], ct[b], N)
+        if int(r["iters"][b]) == info.iters:
+            assert dX <= 0.1 and dF <= 15.0 and dM <= 3.0, (b, dX, dF, dM)
+        assert dX <= 0.3, (b, dX)
+        sc = max(1.0, abs(inst.exact_obj()))
+        assert abs(inst.obj(ub) - inst.obj(xf)) <= 5e-3 * sc, b
 
 
 def test_srbd_literal_edge_cases_and_modes():
