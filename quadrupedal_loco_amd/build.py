@@ -21,6 +21,7 @@ ARCH = "gfx950"
 SOURCES = [
     "qloco_capi.hip",
     "qloco_srbd.hip",
+    "qloco_srbd_lit.hip",
     "qloco_srbd_build.hip",
     "qloco_kin.hip",
     "qloco_gi.hip",
@@ -42,7 +43,8 @@ SOURCES = [
 # loops are unrolled in full (static register per pivot column); the two-wave
 # inverse's body exceeds the default pragma-unroll budget, so it is raised.
 EXTRA = {"qloco_a1qp.hip": ["-ffp-contract=off"], "qloco_gi.hip": ["-ffp-contract=off"], "qloco_gi_wide.hip": ["-ffp-contract=off"], "qloco_force.hip": ["-ffp-contract=off"],
-         "qloco_body.hip": ["-ffp-contract=off"], "qloco_rt.hip": ["-ffp-contract=off"], "qloco_servo.hip": ["-ffp-contract=off"], "qloco_kin.hip": ["-ffp-contract=off"], "qloco_srbd.hip": ["-fno-slp-vectorize", "-mllvm", "-pragma-unroll-threshold=200000"]}
+         "qloco_body.hip": ["-ffp-contract=off"], "qloco_rt.hip": ["-ffp-contract=off"], "qloco_servo.hip": ["-ffp-contract=off"], "qloco_kin.hip": ["-ffp-contract=off"], "qloco_srbd.hip": ["-fno-slp-vectorize", "-mllvm", "-pragma-unroll-threshold=200000"],
+         "qloco_srbd_lit.hip": ["-fno-slp-vectorize", "-mllvm", "-pragma-unroll-threshold=200000"]}
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC]
 

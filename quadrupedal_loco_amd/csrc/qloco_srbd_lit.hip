@@ -1,0 +1,1144 @@
+// qloco_srbd_lit.hip -- the reference's LITERAL 12N-variable SRBD QP for
+// N <= 10 (every (step, leg) pair an ADMM variable, swing legs held by their
+// fz in [0, 0] rows: A1RobotControl.cpp:557-578, ConvexMpc.cpp:162-264),
+// one wavefront per instance, the OSQP linear solve through the per-step
+// wrench space (dispatched by qloco_srbd_solve_ex, qloco_srbd.hip).
+//
+// Why the wrench space.  The forces enter the SRBD dynamics
+// only through each step's wrench increment w_j = Bb u_j (Bb: the omega / v
+// rows of B_d, 6 x 12), so the condensed Hessian is H = Vu' G Vu + R with
+// Vu = I_N (x) Bb and G = K0 (x) Qb + K2 (x) Te (6N x 6N, the closed-form
+// horizon sums of DESIGN.md §3).  OSQP's reduced KKT matrix factors as
+//   K = P~ + sigma I + A~' rho A~ = D [c Vu' G Vu + W0] D,
+//   W0 = c R + D^-1 (sigma I + A~' rho A~) D^-1   (3 x 3 per (step, leg)),
+// and by the push-through identity
+//   K^-1 b = D^-1 (a - W0^-1 Vu' T Vu a),  a = W0^-1 D^-1 b,
+//   T = (I + cG U)^-1 cG = (cG) L S^-1 L^-1   (symmetric, 6N x 6N),
+//   U = Vu W0^-1 Vu' = L L' (6 x 6 per step),  S = I + L' (cG) L  (SPD, >= I).
+// The 120-variable KKT inverse of the two-wave kernel (a 120 x 120 Gauss-
+// Jordan, 2 x 124 register columns per lane) becomes a 60 x 60 inverse of the
+// well-conditioned S (eigenvalues >= 1, so pivot-free Gauss-Jordan is
+// stable) plus a 60 x 60 product, and each ADMM iteration a 60 x 60 matvec
+// plus leg-local 3 x 3 blocks and per-step wrench sums -- one wave, 60
+// register columns.  Same arithmetic as OSQP up to rounding
+// (tools/proto_lit.py: float64 iterates agree to 1e-10, a float32 solve to
+// 4e-7 relative; iteration counts equal on every instance tried).
+//
+// Lane l holds two variables (slot h = 0, 1: v = 60 h + l, l < 60; step
+// v / 12, leg (v % 12) / 3, component v % 3 -- leg triples never straddle),
+// their <= 2 constraint rows each (as the two-wave kernel), and wrench row
+// r = l (step l / 6, component l % 6: 0..2 omega, 3..5 v).
+#include <math.h>
+
+#include <type_traits>
+
+#include "qloco_srbd_core.hpp"
+
+namespace qloco {
+
+constexpr int kLitWpe = 3;  // waves per SIMD: 168 VGPRs, <= 13.3 KB of LDS (static_assert below)
+
+struct LitLds {
+  f4v bc[2][16];            // broadcast ring: 60-vectors read as one 16-B chunk per lane
+  float av[2][64];          // per-slot exchange (a, D x, t)
+  float wv[64];             // wrench rows (s, w)
+  float tw[64];             // wrench rows (Te w)
+  f2v k0k2[kLitN][kLitN];   // horizon sums K0 / K2 (row step, column step)
+  float Bb[6][12];          // wrench map (constant feet), rows omega 0..2, v 3..5
+  float Te[6][6];           // dt^2 blockdiag(Rz' Qtheta Rz, Qp)
+  float q2[16], r2[12], x0[16];
+  float ctf[4 * kLitN];     // contact flags as floats
+  f2v zb[2][64];            // per slot: scaled bounds of row 0 (row 1: [-inf, 0])
+  f4v arz[2][64];           // per slot: scaled A entries (ra0, ra1, rz0, rz1)
+  union {                   // phase-local storage (LDS bounds the occupancy: <= 20 KB)
+    struct {                // gradient + Ruiz
+      f2v beps[12][12];     // (beta, eps)[w][w']: the P entries' per-column coefficients
+      float dcol[120];      // Ruiz column scales D (read as same-address broadcasts)
+      float err[12 * kLitN];  // gradient scans
+      float Wc[12 * kLitN];
+    };
+    struct {                // factorisation
+      f4v w0i[2][64];       // per variable: its row of W0^-1 (x, y, z) + pad
+      float TL[kLitN][6][6];  // per step: rows of Te L_j
+      float Lt[kLitN][21];    // per step: columns of L_j, packed (column t: rows t..5 at tri(t))
+      float Li[kLitN][21];    // per step: columns of L_j^-1, packed the same way
+      union {
+        float U[kLitN][6][6];  // per step: U_j (until its Cholesky)
+        struct {
+          f4v zc[64], tc[64];  // T passes: Z (then L Z, same wave, in order), Te L Z columns
+        };
+      };
+    };
+  };
+};
+static_assert(sizeof(LitLds) <= 13653, "literal kernel: three workgroups per SIMD need <= 160 KB / 12 of LDS");
+
+// Compile-time loop over columns C..E-1 (the DPP control of a column's
+// broadcast must be a constant expression).
+template <int C, int E>
+struct ColLoop {
+  template <class F>
+  static __device__ __forceinline__ void run(F &&f) {
+    f(std::integral_constant<int, C>{});
+    ColLoop<C + 1, E>::run(f);
+  }
+};
+template <int E>
+struct ColLoop<E, E> {
+  template <class F>
+  static __device__ __forceinline__ void run(F &&) {}
+};
+// Column c of a 60-vector read as one 16-byte chunk per lane (lane l holds
+// elements 4(l % 16) .. +3): DPP row_newbcast:(c / 4) of component c % 4.
+template <int C>
+__device__ __forceinline__ float dpp_col(const f4v &d) {
+  constexpr int e = C & 3;
+  const float v = e == 0 ? d.x : (e == 1 ? d.y : (e == 2 ? d.z : d.w));
+  return dpp<0x150 + (C >> 2)>(v);
+}
+
+// Packed lower-triangular 6 x 6 columns: column t (rows t..5) starts at
+// tri(t); tri(t) - t + s addresses row s >= t.
+__device__ __forceinline__ constexpr int tri(int t) { return 6 * t - (t * (t - 1)) / 2; }
+
+// Wave-level helpers for the one-wave literal kernel
+__device__ __forceinline__ void lsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The three entries of this lane's leg triple (components 0, 1, 2) of a
+// per-lane value: lanes 3m, 3m+1, 3m+2 hold one leg.
+struct Triple {
+  float v0, v1, v2;
+};
+__device__ __forceinline__ Triple triple(float v, int comp) {
+  const float n1 = lane_next(v), n2 = lane_next(n1);
+  const float p1 = lane_prev(v), p2 = lane_prev(p1);
+  Triple t;
+  t.v0 = comp == 0 ? v : (comp == 1 ? p1 : p2);
+  t.v1 = comp == 0 ? n1 : (comp == 1 ? v : p1);
+  t.v2 = comp == 0 ? n2 : (comp == 1 ? n1 : v);
+  return t;
+}
+
+// In-place Gauss-Jordan inverse of the 60 x 60 SPD S (one row per lane,
+// eigenvalues >= 1): invert_w1's scheme on the literal LDS.
+__device__ __forceinline__ void lit_invert(LitLds &S, int lane, int ncol, Row<1> &K) {
+  int nc = __builtin_amdgcn_readfirstlane(ncol);
+#pragma unroll
+  for (int k = 0; k < 60; ++k) {
+    asm volatile("" : "+s"(nc));
+    if (k >= nc) continue;
+    float *bcf = reinterpret_cast<float *>(&S.bc[k & 1][0]);
+    int tt = lane;
+    asm volatile("" : "+v"(tt));
+    const float v = K.k[k];
+    const float p = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
+    bcf[tt] = (tt == k) ? p + 1.0f : ((tt < k) ? -v : v);
+    lsync();
+    const f4v r0 = S.bc[k & 1][lane & 15];
+    const float pinv = __builtin_amdgcn_rcpf(p);
+    const float ng = -((tt == k) ? (1.0f - pinv) : v * pinv);
+    QL_DPP_GJ60(K.k, 0, r0, ng);
+    if (p > kGjExactPivot) K.k[k] = (tt == k) ? pinv : ng;
+  }
+  lsync();
+}
+
+// 6 x 6 Cholesky L L' = A (lower, row-major a[r][c]) and L^-1, all in
+// registers (every lane of a step computes the same factor).
+__device__ __forceinline__ void chol6(const float (&a)[6][6], float (&L)[6][6], float (&Li)[6][6]) {
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) L[r][c] = 0.0f, Li[r][c] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float d = a[i][i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) d = fmaf(-L[i][k], L[i][k], d);
+    d = fmaxf(d, 1e-30f);
+    const float li = __builtin_amdgcn_rsqf(d);
+    L[i][i] = d * li;
+#pragma unroll
+    for (int r = i + 1; r < 6; ++r) {
+      float s = a[r][i];
+#pragma unroll
+      for (int k = 0; k < i; ++k) s = fmaf(-L[r][k], L[i][k], s);
+      L[r][i] = s * li;
+    }
+  }
+  // L^-1 (lower): forward substitution on the unit columns
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+#pragma unroll
+    for (int r = c; r < 6; ++r) {
+      float s = r == c ? 1.0f : 0.0f;
+#pragma unroll
+      for (int k = c; k < r; ++k) s = fmaf(-L[r][k], Li[k][c], s);
+      Li[r][c] = s / L[r][r];
+    }
+  }
+}
+
+// WS: a warm-start mode (1 or 2) may be set (the persistent record of
+// DESIGN.md §3c, literal semantics: the update path on every call).
+template <bool WS>
+__device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const int64_t b) {
+  const int lane = threadIdx.x;
+  const int N = a.N;
+  const float Nf = (float)N;
+  const float dt = a.dt;
+  const float dtm = dt / a.mass, dt2m = dt * dt / a.mass;
+  const int nvar = 12 * N, nw = 6 * N;
+
+  // ---------------- 1. inputs -> LDS
+  if (lane < 13) S.x0[lane] = a.x0[b * 13 + lane];
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 13; ++k) S.q2[k] = a.q2[k];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) S.r2[k] = a.r2[k];
+  }
+  {
+    const int nct = a.contacts_per_step ? 4 * N : 4;
+    if (lane < 4 * N) S.ctf[lane] = a.contacts[b * nct + (a.contacts_per_step ? lane : (lane & 3))] ? 1.0f : 0.0f;
+  }
+  for (int idx = lane; idx < kLitN * kLitN; idx += 64) {
+    const int sr = idx / kLitN, sc = idx - kLitN * sr;
+    float K0 = 0.0f, K2 = 0.0f;
+    if (sr < N && sc < N) k0k2((float)sr, (float)sc, Nf, K0, K2);
+    S.k0k2[sr][sc] = (f2v){K0, K2};
+  }
+  lsync();
+
+  // ---------------- 2. SRBD model (ConvexMpc.cpp:111-160, compute_grf :502-549)
+  const float yaw = S.x0[2];
+  const float cy = cosf(yaw), sy = sinf(yaw);
+  const float R00 = cy, R01 = sy, R10 = -sy, R11 = cy;  // A1RobotControl.cpp:506-508
+  float Ii[3][3];
+  {
+    const float *I = a.inertia;
+    const float Rm[3][3] = {{R00, R01, 0.f}, {R10, R11, 0.f}, {0.f, 0.f, 1.f}};
+    float RI[3][3], Iw[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        RI[r][c] = Rm[r][0] * I[c * 3 + 0] + Rm[r][1] * I[c * 3 + 1] + Rm[r][2] * I[c * 3 + 2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        Iw[r][c] = RI[r][0] * Rm[c][0] + RI[r][1] * Rm[c][1] + RI[r][2] * Rm[c][2];
+    const float c00 = Iw[1][1] * Iw[2][2] - Iw[1][2] * Iw[2][1];
+    const float c01 = Iw[1][2] * Iw[2][0] - Iw[1][0] * Iw[2][2];
+    const float c02 = Iw[1][0] * Iw[2][1] - Iw[1][1] * Iw[2][0];
+    const float id = 1.0f / (Iw[0][0] * c00 + Iw[0][1] * c01 + Iw[0][2] * c02);
+    Ii[0][0] = c00 * id;
+    Ii[1][0] = c01 * id;
+    Ii[2][0] = c02 * id;
+    Ii[0][1] = (Iw[0][2] * Iw[2][1] - Iw[0][1] * Iw[2][2]) * id;
+    Ii[1][1] = (Iw[0][0] * Iw[2][2] - Iw[0][2] * Iw[2][0]) * id;
+    Ii[2][1] = (Iw[0][1] * Iw[2][0] - Iw[0][0] * Iw[2][1]) * id;
+    Ii[0][2] = (Iw[0][1] * Iw[1][2] - Iw[0][2] * Iw[1][1]) * id;
+    Ii[1][2] = (Iw[0][2] * Iw[1][0] - Iw[0][0] * Iw[1][2]) * id;
+    Ii[2][2] = (Iw[0][0] * Iw[1][1] - Iw[0][1] * Iw[1][0]) * id;
+  }
+  // per slot: the variable, its B_d column (omega rows: ba) and E column
+  const int comp = lane % 3;
+  const bool xy = comp < 2;
+  bool valid[2];
+  int step[2], leg[2];
+  f4v lo[2], hi[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int v = 60 * h + lane;
+    valid[h] = lane < 60 && v < nvar;
+    step[h] = valid[h] ? v / 12 : 0;
+    leg[h] = valid[h] ? (v % 12) / 3 : 0;
+    const float *rf = a.feet + b * 12 + 3 * leg[h];
+    const float rx = rf[0], ry = rf[1], rz = rf[2];
+    const float tv0 = comp == 0 ? 0.f : (comp == 1 ? -rz : ry);  // skew(r) e_comp (Utils.cpp:35-41)
+    const float tv1 = comp == 0 ? rz : (comp == 1 ? 0.f : -rx);
+    const float tv2 = comp == 0 ? -ry : (comp == 1 ? rx : 0.f);
+    float ba[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) ba[r] = dt * (Ii[r][0] * tv0 + Ii[r][1] * tv1 + Ii[r][2] * tv2);
+    lo[h] = (f4v){ba[0], ba[1], ba[2], dt * (R00 * ba[0] + R01 * ba[1])};
+    hi[h] = (f4v){dt * (R10 * ba[0] + R11 * ba[1]), dt * ba[2], (float)step[h], (float)comp};
+    if (!valid[h]) {
+      lo[h] = (f4v)(0.0f);
+      hi[h] = (f4v){0.0f, 0.0f, 0.0f, -1.0f};
+    }
+    // the wrench map (constant feet): column v % 12 of Bb from the step-0 lanes
+    if (h == 0 && lane < 12) {
+      S.Bb[0][lane] = ba[0];
+      S.Bb[1][lane] = ba[1];
+      S.Bb[2][lane] = ba[2];
+      S.Bb[3][lane] = comp == 0 ? dtm : 0.0f;
+      S.Bb[4][lane] = comp == 1 ? dtm : 0.0f;
+      S.Bb[5][lane] = comp == 2 ? dtm : 0.0f;
+    }
+  }
+  // Te = dt^2 blockdiag(Rz' diag(q2[0:3]) Rz, diag(q2[3:6]))
+  if (lane < 36) {
+    const int r = lane / 6, c = lane - 6 * (lane / 6);
+    const float Rm[3][3] = {{R00, R01, 0.f}, {R10, R11, 0.f}, {0.f, 0.f, 1.f}};
+    float v = 0.0f;
+    if (r < 3 && c < 3)
+      v = dt * dt * (Rm[0][r] * S.q2[0] * Rm[0][c] + Rm[1][r] * S.q2[1] * Rm[1][c] + Rm[2][r] * S.q2[2] * Rm[2][c]);
+    else if (r >= 3 && c == r)
+      v = dt * dt * S.q2[r];
+    S.Te[r][c] = v;
+  }
+  float r2v[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) r2v[h] = valid[h] ? S.r2[3 * leg[h] + comp] : 0.0f;
+
+  // ---------------- 3. gradient g = Bqp' Q (Aqp x0 - x_ref) (ConvexMpc.cpp:219-221)
+  for (int idx = lane; idx < 12 * N; idx += 64) {
+    const int i = idx / 12, s = idx - 12 * i;
+    const float k = (float)(i + 1);
+    const float *x0 = S.x0;
+    float xf;
+    if (s < 3) {
+      const float rw = s == 0 ? (R00 * x0[6] + R01 * x0[7]) : (s == 1 ? (R10 * x0[6] + R11 * x0[7]) : x0[8]);
+      xf = x0[s] + k * dt * rw;
+    } else if (s < 6) {
+      xf = x0[s] + k * dt * x0[s + 6];
+      if (s == 5) xf += 0.5f * k * (k - 1.0f) * dt * dt * x0[12];
+    } else if (s < 9) {
+      xf = x0[s];
+    } else {
+      xf = x0[s] + (s == 11 ? k * dt * x0[12] : 0.0f);
+    }
+    S.err[idx] = S.q2[s] * (xf - a.xref[b * 13 * N + 13 * i + s]);
+  }
+  lsync();
+  if (lane < 12) {  // suffix scans per state row (row_scans of the two-wave kernel)
+    const int r = lane;
+    const bool brow = r >= 6;
+    float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+    for (int j = kLitN - 1; j >= 0; --j) {
+      if (j < N) {
+        s1 += s0;
+        s0 += S.err[12 * j + r];
+        S.Wc[12 * j + r] = brow ? s0 : s1;
+      }
+    }
+  }
+  lsync();
+  float qv[2], qsv[2], q_raw[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float g = 0.0f;
+    if (valid[h]) {
+      const float *w = S.Wc + 12 * step[h];
+      g = lo[h].x * w[6] + lo[h].y * w[7] + lo[h].z * w[8];
+      g += lo[h].w * w[0] + hi[h].x * w[1] + hi[h].y * w[2];
+      g += dtm * w[9 + comp] + dt2m * w[3 + comp];
+    }
+    qv[h] = g;
+    q_raw[h] = g;
+    qsv[h] = g;
+  }
+  // from here on a variable's B_d column is all the iterations need of lo/hi:
+  // its omega rows (the wrench map's torque part; the force part is dtm e_comp)
+  float bwo[2][3];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bwo[h][0] = lo[h].x;
+    bwo[h][1] = lo[h].y;
+    bwo[h][2] = lo[h].z;
+  }
+  // persistent solver (warm_start == 2): literal semantics -- after the
+  // first call every call takes OSQP's update path
+  const int NP = 100 * N;
+  float *prec = (WS && a.warm_start == 2) ? a.warm + b * (int64_t)(NP + 4) : nullptr;
+  bool p_init = false;
+  if (prec) p_init = prec[NP + 1] > 0.5f;
+  const bool p_same = p_init;
+  if (p_same) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (valid[h]) qsv[h] = prec[84 * N + 12 * step[h] + 3 * leg[h] + comp];
+  }
+
+  // ---------------- 4. constraint rows owned by each slot (ConvexMpc.cpp:47-59, :227-249)
+  float ra0[2], ra1[2], rz0[2], rz1[2], rl0[2], ru0[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    ra0[h] = valid[h] ? 1.0f : 0.0f;
+    ra1[h] = (valid[h] && xy) ? 1.0f : 0.0f;
+    rz0[h] = (valid[h] && xy) ? a.mu : 0.0f;
+    rz1[h] = (valid[h] && xy) ? -a.mu : 0.0f;
+    const float cflag = valid[h] ? S.ctf[4 * step[h] + leg[h]] : 0.0f;
+    rl0[h] = !valid[h] ? 0.0f : (xy ? 0.0f : a.fz_min * cflag);
+    ru0[h] = !valid[h] ? 0.0f : (xy ? INFINITY : a.fz_max * cflag);
+  }
+
+  // ---------------- 5. modified Ruiz equilibration (OSQP scaling.c), P rows
+  // generated from the wrench structure: P[(j,w),(k,w')] = K0(j,k) beta[w][w']
+  // + K2(j,k) eps[w][w'] + R delta, beta = <b_w, b_w'>_Qb, eps = <b_w, b_w'>_Te
+  float rE0[2] = {1.0f, 1.0f}, rE1[2] = {1.0f, 1.0f}, Dr[2] = {1.0f, 1.0f}, cs = 1.0f;
+  {
+    // beta / eps tables (12 x 12, constant feet) in LDS: beta[w][w'] =
+    // sum_s Qb_s Bb[s][w] Bb[s][w'], eps[w][w'] = Bb[:,w]' Te Bb[:,w']
+    lsync();
+    for (int e = lane; e < 144; e += 64) {
+      const int w = e / 12, wp = e - 12 * (e / 12);
+      float bb = 0.0f, ee = 0.0f;
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        bb = fmaf(S.q2[6 + s] * S.Bb[s][w], S.Bb[s][wp], bb);
+        float tw = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 6; ++t) tw = fmaf(S.Te[s][t], S.Bb[t][wp], tw);
+        ee = fmaf(S.Bb[s][w], tw, ee);
+      }
+      S.beps[w][wp] = (f2v){bb, ee};
+    }
+    lsync();
+    // this lane's diagonal P entries (R included)
+    float pdiag[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int wl = valid[h] ? (60 * h + lane) % 12 : 0;
+      const f2v kk = S.k0k2[step[h]][step[h]];
+      const f2v be = S.beps[wl][wl];
+      pdiag[h] = valid[h] ? fmaf(kk.y, be.y, kk.x * be.x) + r2v[h] : 0.0f;
+    }
+    // this lane's (beta, eps) rows, per slot (registers for the whole of
+    // Ruiz: every column step reuses them)
+    float bet[2][12], eps[2][12];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int wl = h == 0 ? (valid[0] ? lane % 12 : 0) : (valid[1] ? (60 + lane) % 12 : 0);
+#pragma unroll
+      for (int w = 0; w < 12; ++w) {
+        const f2v be = S.beps[wl][w];
+        bet[h][w] = valid[h] ? be.x : 0.0f;
+        eps[h][w] = valid[h] ? be.y : 0.0f;
+      }
+    }
+    // row inf-norms |P_vc| D_c of both slots' rows in one sweep over the 120
+    // columns, step-major: per column step the K0 / K2 weights of the two
+    // rows' steps and the step's 12 column scales (same-address LDS reads,
+    // a broadcast), then 12 entries per row from the (beta, eps) rows
+    auto row_norms = [&](bool scaled, float (&m)[2]) {
+      // loop-invariant tables: opaque per call (no hoisting of all 240 entries)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int w = 0; w < 12; ++w) asm volatile("" : "+v"(bet[h][w]), "+v"(eps[h][w]));
+      float m0 = 0.0f, m1 = 0.0f;
+#pragma unroll
+      for (int kc = 0; kc < kLitN; ++kc) {
+        asm volatile("" ::: "memory");  // table reads stay in the pass (no LICM)
+        __builtin_amdgcn_sched_barrier(0);
+        const f2v k0 = S.k0k2[step[0]][kc], k1 = S.k0k2[step[1]][kc];
+        const f4v *dc = reinterpret_cast<const f4v *>(&S.dcol[12 * kc]);
+        const f4v da = scaled ? dc[0] : (f4v)(1.0f), db = scaled ? dc[1] : (f4v)(1.0f),
+                  dd = scaled ? dc[2] : (f4v)(1.0f);
+        const float dv[12] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w, dd.x, dd.y, dd.z, dd.w};
+#pragma unroll
+        for (int w = 0; w < 12; ++w) {
+          const float p0 = fmaf(k0.y, eps[0][w], k0.x * bet[0][w]);
+          const float p1 = fmaf(k1.y, eps[1][w], k1.x * bet[1][w]);
+          m0 = fmaxf(m0, fabsf(p0) * dv[w]);
+          m1 = fmaxf(m1, fabsf(p1) * dv[w]);
+        }
+        // pin the step's arithmetic here (no sinking into a late masked block
+        // that would keep every step's loads live)
+        asm volatile("" : "+v"(m0), "+v"(m1));
+      }
+      m[0] = valid[0] ? m0 : 0.0f;
+      m[1] = valid[1] ? m1 : 0.0f;
+    };
+    float cnP[2];
+    {
+      float m[2];
+      row_norms(false, m);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) cnP[h] = valid[h] ? fmaxf(m[h], pdiag[h]) : 0.0f;
+    }
+    const float inv_n = 1.0f / (float)nvar;
+    for (int it = 0; it < a.scaling; ++it) {
+      float Dt[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float cnA = fmaxf(fabsf(ra0[h]), fabsf(ra1[h]));
+        const float zmax = fmaxf(fabsf(rz0[h]), fabsf(rz1[h]));
+        const float zm1 = lane_prev(zmax), zm2 = lane_prev(zm1);
+        if (comp == 2) cnA = fmaxf(cnA, fmaxf(zm1, zm2));
+        Dt[h] = valid[h] ? __builtin_amdgcn_rsqf(limit_scaling(fmaxf(cnP[h], cnA))) : 1.0f;
+        const float Et0 = valid[h] ? __builtin_amdgcn_rsqf(limit_scaling(fmaxf(fabsf(ra0[h]), fabsf(rz0[h])))) : 1.0f;
+        const float Et1 = (valid[h] && xy) ? __builtin_amdgcn_rsqf(limit_scaling(fmaxf(fabsf(ra1[h]), fabsf(rz1[h])))) : 1.0f;
+        const float Dn1 = lane_next(Dt[h]), Dn2 = lane_next(Dn1);
+        const float Dz = comp == 0 ? Dn2 : (comp == 1 ? Dn1 : Dt[h]);
+        ra0[h] *= Et0 * Dt[h];
+        ra1[h] *= Et1 * Dt[h];
+        rz0[h] *= Et0 * Dz;
+        rz1[h] *= Et1 * Dz;
+        rE0[h] *= Et0;
+        rE1[h] *= Et1;
+        qv[h] *= Dt[h];
+        qsv[h] *= Dt[h];
+        Dr[h] *= Dt[h];
+        if (lane < 60) S.dcol[60 * h + lane] = valid[h] ? Dr[h] : 0.0f;
+      }
+      lsync();
+      float cn2[2], mr[2];
+      row_norms(true, mr);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) cn2[h] = valid[h] ? Dr[h] * fmaxf(mr[h], pdiag[h] * Dr[h]) : 0.0f;
+      // cost scaling: mean column norm of the scaled P vs ||q||_inf
+      const float sumP = wsum(cn2[0] + cn2[1]);
+      const float qm = wmax_nonneg(fmaxf(valid[0] ? fabsf(qsv[0]) : 0.0f, valid[1] ? fabsf(qsv[1]) : 0.0f));
+      const float meanP = cs * sumP * inv_n;
+      const float ctc = __builtin_amdgcn_rcpf(limit_scaling(fmaxf(meanP, limit_scaling(qm))));
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        qv[h] *= ctc;
+        qsv[h] *= ctc;
+        cnP[h] = cn2[h] * cs * ctc;
+      }
+      cs *= ctc;
+      lsync();
+    }
+  }
+  const float cinv = 1.0f / cs;
+  bool eq0[2];
+  float qn[2] = {0.0f, 0.0f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float lh0 = rl0[h] * rE0[h], uh0 = ru0[h] * rE0[h];
+    eq0[h] = valid[h] && !xy && (uh0 - lh0 < 1e-4f);  // OSQP set_rho_vec: RHO_TOL
+    S.zb[h][lane] = (f2v){lh0, uh0};
+    S.arz[h][lane] = (f4v){ra0[h], ra1[h], rz0[h], rz1[h]};
+    qn[0] = fmaxf(qn[0], valid[h] ? fabsf(qv[h] / Dr[h]) : 0.0f);
+    qn[1] = fmaxf(qn[1], valid[h] ? fabsf(qv[h]) : 0.0f);
+  }
+  qn[0] = wmax_nonneg(qn[0]);
+  qn[1] = wmax_nonneg(qn[1]);
+  lsync();
+
+  // row scaling E of a slot's two rows, from A~ = E A D (each row's entry in
+  // its own variable's column is 1 before scaling)
+  auto row_e = [&](int h) -> f2v {
+    const f4v arz = S.arz[h][lane];
+    const float d = Dr[h];
+    return (f2v){valid[h] ? arz.x / d : 1.0f, (valid[h] && xy) ? arz.y / d : 1.0f};
+  };
+
+  // wrench row of this lane: step jr, component sr; its row of Bb (12)
+  const bool wvalid = lane < nw;
+  // lanes 6N..59 carry the (identity) factors of the padding steps, whose
+  // K0 / K2 weights are zero; lanes 60..63 only pad
+  const int jr = lane < 60 ? lane / 6 : kLitN - 1, sr = lane < 60 ? lane - 6 * (lane / 6) : 0;
+  // this lane's row of Bb (12) is read from LDS where used (registers are
+  // the factorisation's bound); padding wrench lanes get zeros
+  // through their K0 / K2 weights and masks
+  // this lane's variables' wrench columns (omega rows = lo.xyz, v row = dtm at comp)
+  float rho = fminf(fmaxf(p_same ? prec[NP] : a.rho, 1e-6f), 1e6f);
+
+  // ---------------- 6. ADMM (osqp_solve) with its (re)factorisations
+  float x[2] = {0.0f, 0.0f};
+  f2v z[2] = {(f2v)(0.0f), (f2v)(0.0f)}, y[2] = {(f2v)(0.0f), (f2v)(0.0f)};
+  const float alpha = a.alpha, oma = 1.0f - a.alpha, sigma = a.sigma;
+  const int ctm = a.check_termination;
+  const int interval = (a.adaptive_rho && a.rho_interval == 0) ? (ctm ? 4 * ctm : 100)
+                                                               : (a.adaptive_rho ? a.rho_interval : 0);
+  int status = QLOCO_MAX_ITER, iter = 0, rho_updates = 0;
+  float px[2] = {0.0f, 0.0f};
+  Row<1> T;        // T = (I + cG U)^-1 cG, this lane's wrench row
+  float A1[2][3], B1[2][3], Dinv[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) Dinv[h] = valid[h] ? 1.0f / Dr[h] : 0.0f;
+
+  // P~ x (scaled) per slot: c D (Vu' G Vu + R) D x through the wrench rows
+  auto p_times_x = [&](float (&out)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) S.av[h][lane] = valid[h] ? x[h] * Dr[h] : 0.0f;
+    lsync();
+    // w = Vu (D x): wrench row (jr, sr) sums its step's 12 variables
+    float wr = 0.0f;
+    {
+      const int hh = jr >= 5 ? 1 : 0, base = 12 * (jr - 5 * hh);
+      const f4v *src = reinterpret_cast<const f4v *>(&S.av[hh][base]);
+      const f4v u0 = src[0], u1 = src[1], u2 = src[2];
+      const float uv[12] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w, u2.x, u2.y, u2.z, u2.w};
+      const f4v *br = reinterpret_cast<const f4v *>(S.Bb[sr]);
+      const f4v b0 = br[0], b1 = br[1], b2 = br[2];
+      const float bv[12] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w};
+#pragma unroll
+      for (int w = 0; w < 12; ++w) wr = fmaf(bv[w], uv[w], wr);
+      wr = wvalid ? wr : 0.0f;
+    }
+    S.wv[lane] = wr;
+    lsync();
+    // Te w per row (needs the step's 6 wrench values)
+    {
+      float tw = 0.0f;
+#pragma unroll
+      for (int t = 0; t < 6; ++t) tw = fmaf(S.Te[sr][t], S.wv[6 * jr + t], tw);
+      S.tw[lane] = wvalid ? tw : 0.0f;
+    }
+    lsync();
+    // (G w)[(jr, sr)] = Qb_s sum_k K0(jr,k) w(k,sr) + sum_k K2(jr,k) (Te w_k)_sr
+    float gw = 0.0f;
+    {
+      const float qb = S.q2[6 + sr];
+      float s0 = 0.0f, s2 = 0.0f;
+#pragma unroll
+      for (int k = 0; k < kLitN; ++k) {
+        const f2v kk = S.k0k2[jr][k];
+        s0 = fmaf(kk.x, S.wv[6 * k + sr], s0);
+        s2 = fmaf(kk.y, S.tw[6 * k + sr], s2);
+      }
+      gw = wvalid ? fmaf(qb, s0, s2) : 0.0f;
+    }
+    lsync();
+    S.wv[lane] = gw;
+    lsync();
+    // Vu' (G w) + R (D x), then c D (...)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float acc = 0.0f;
+      if (valid[h]) {
+        const float *gs = &S.wv[6 * step[h]];
+        acc = bwo[h][0] * gs[0] + bwo[h][1] * gs[1] + bwo[h][2] * gs[2] + dtm * gs[3 + comp];
+        acc = fmaf(r2v[h], x[h] * Dr[h], acc);
+      }
+      out[h] = cs * Dr[h] * acc;
+    }
+    lsync();
+  };
+
+  auto residuals = [&](float (&o)[6], float (&r)[6], bool want_r) {
+    p_times_x(px);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) o[k] = r[k] = 0.0f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float Drl = Dr[h];
+      const float Dinvl = __builtin_amdgcn_rcpf(Drl);
+      const f4v arz = S.arz[h][lane];
+      // E^-1 of the slot's rows from A~ = E A D (unit own-column entries)
+      const f2v Einv = {valid[h] ? Drl * __builtin_amdgcn_rcpf(arz.x) : 1.0f,
+                        (valid[h] && xy) ? Drl * __builtin_amdgcn_rcpf(arz.y) : 1.0f};
+      const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
+      const float n1 = lane_next(x[h]), n2 = lane_next(n1);
+      const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x[h]);
+      const f2v ay = ra * y[h], az = rz * y[h];
+      const float ay_z = az.x + az.y;
+      const float p1 = lane_prev(ay_z), p2 = lane_prev(p1);
+      const float aty = valid[h] ? ((ay.x + ay.y) + (comp == 2 ? (p1 + p2) : 0.0f)) : 0.0f;
+      const float rd = valid[h] ? (qv[h] + px[h] + aty) : 0.0f;
+      const f2v ax = ra * x[h] + rz * xz;
+      const f2v rp = ax - z[h];
+      const f2v erp = Einv * rp, ez = Einv * z[h], eax = Einv * ax;
+      o[0] = fmaxf(o[0], fmaxf(fabsf(erp.x), fabsf(erp.y)));
+      o[1] = fmaxf(o[1], fmaxf(fabsf(ez.x), fabsf(ez.y)));
+      o[2] = fmaxf(o[2], fmaxf(fabsf(eax.x), fabsf(eax.y)));
+      o[3] = fmaxf(o[3], fabsf(Dinvl * rd));
+      o[4] = fmaxf(o[4], fabsf(Dinvl * aty));
+      o[5] = fmaxf(o[5], fabsf(Dinvl * px[h]));
+      if (want_r) {
+        r[0] = fmaxf(r[0], fmaxf(fabsf(rp.x), fabsf(rp.y)));
+        r[1] = fmaxf(r[1], fmaxf(fabsf(z[h].x), fabsf(z[h].y)));
+        r[2] = fmaxf(r[2], fmaxf(fabsf(ax.x), fabsf(ax.y)));
+        r[3] = fmaxf(r[3], fabsf(rd));
+        r[4] = fmaxf(r[4], fabsf(aty));
+        r[5] = fmaxf(r[5], fabsf(px[h]));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) o[k] = wmax_nonneg(o[k]);
+    if (want_r) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) r[k] = wmax_nonneg(r[k]);
+    }
+  };
+
+  // warm start (x, z, y) before the first factorisation
+  if (WS) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int vidx = 12 * step[h] + 3 * leg[h] + comp, rbase = 20 * step[h] + 5 * leg[h] + 2 * comp;
+      if (p_same) {
+        x[h] = valid[h] ? prec[vidx] : 0.0f;
+        z[h].x = valid[h] ? prec[12 * N + rbase] : 0.0f;
+        z[h].y = (valid[h] && xy) ? prec[12 * N + rbase + 1] : 0.0f;
+        y[h].x = valid[h] ? prec[32 * N + rbase] : 0.0f;
+        y[h].y = (valid[h] && xy) ? prec[32 * N + rbase + 1] : 0.0f;
+      } else if (a.warm_start == 1) {
+        const float *wx = a.warm + b * (32 * N);
+        const float *wy = wx + 12 * N;
+        x[h] = valid[h] ? wx[vidx] / Dr[h] : 0.0f;
+        const f2v e = row_e(h);
+        y[h].x = valid[h] ? wy[rbase] / e.x * cs : 0.0f;
+        y[h].y = (valid[h] && xy) ? wy[rbase + 1] / e.y * cs : 0.0f;
+        const float n1 = lane_next(x[h]), n2 = lane_next(n1);
+        const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x[h]);
+        const f4v arz = S.arz[h][lane];
+        z[h] = (f2v){arz.x, arz.y} * x[h] + (f2v){arz.z, arz.w} * xz;
+      }
+    }
+  }
+  for (;;) {
+    // ---------------- 6a. factorisation for the current rho
+    {
+      // opaque per factorisation: nothing derived from these is hoisted out of
+      // the refactor loop (it would stay live through the ADMM iterations)
+      int ln = lane;
+      float csf = cs, dinv[2] = {Dinv[0], Dinv[1]};
+      asm volatile("" : "+v"(ln), "+v"(csf), "+v"(dinv[0]), "+v"(dinv[1]));
+      // W0 rows (D-unscaled leg blocks) and their inverses, per slot
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f4v arz = S.arz[h][lane];
+        const float rv0 = eq0[h] ? 1e3f * rho : rho, rv1 = rho;
+        const float d_own = rv0 * arz.x * arz.x + rv1 * arz.y * arz.y;
+        const float d_oz = rv0 * arz.x * arz.z + rv1 * arz.y * arz.w;
+        const float d_zz = rv0 * arz.z * arz.z + rv1 * arz.w * arz.w;
+        const float oz1 = lane_prev(d_oz), oz2 = lane_prev(oz1);
+        const float zz1 = lane_prev(d_zz), zz2 = lane_prev(zz1);
+        float m0, m1, m2;  // this lane's row of sigma I + A~' rho A~ (scaled space)
+        if (comp == 0) {
+          m0 = d_own + sigma; m1 = 0.0f; m2 = d_oz;
+        } else if (comp == 1) {
+          m0 = 0.0f; m1 = d_own + sigma; m2 = d_oz;
+        } else {
+          m0 = oz2; m1 = oz1; m2 = d_own + zz1 + zz2 + sigma;
+        }
+        const Triple dd = triple(dinv[h], comp);
+        // W0 row = D^-1 M D^-1 + c R (diagonal)
+        float w0 = dinv[h] * m0 * dd.v0, w1 = dinv[h] * m1 * dd.v1, w2 = dinv[h] * m2 * dd.v2;
+        const float cr = csf * r2v[h];
+        w0 += comp == 0 ? cr : 0.0f;
+        w1 += comp == 1 ? cr : 0.0f;
+        w2 += comp == 2 ? cr : 0.0f;
+        if (!valid[h]) { w0 = comp == 0 ? 1.0f : 0.0f; w1 = comp == 1 ? 1.0f : 0.0f; w2 = comp == 2 ? 1.0f : 0.0f; }
+        // the full 3 x 3 leg block: rows from the triple's lanes
+        const Triple c0 = triple(w0, comp), c1 = triple(w1, comp), c2 = triple(w2, comp);
+        // rows: row0 = (c0.v0, c1.v0, c2.v0), row1 = (c0.v1, ...), row2 = (c0.v2, ...)
+        const float a00 = c0.v0, a01 = c1.v0, a02 = c2.v0;
+        const float a10 = c0.v1, a11 = c1.v1, a12 = c2.v1;
+        const float a20 = c0.v2, a21 = c1.v2, a22 = c2.v2;
+        const float k00 = a11 * a22 - a12 * a21, k01 = a02 * a21 - a01 * a22, k02 = a01 * a12 - a02 * a11;
+        const float k10 = a12 * a20 - a10 * a22, k11 = a00 * a22 - a02 * a20, k12 = a02 * a10 - a00 * a12;
+        const float k20 = a10 * a21 - a11 * a20, k21 = a01 * a20 - a00 * a21, k22 = a00 * a11 - a01 * a10;
+        const float idet = 1.0f / (a00 * k00 + a01 * k10 + a02 * k20);
+        const float i0 = (comp == 0 ? k00 : (comp == 1 ? k10 : k20)) * idet;  // row comp of W0^-1
+        const float i1 = (comp == 0 ? k01 : (comp == 1 ? k11 : k21)) * idet;
+        const float i2 = (comp == 0 ? k02 : (comp == 1 ? k12 : k22)) * idet;
+        S.w0i[h][lane] = (f4v){i0, i1, i2, 0.0f};
+      }
+      lsync();
+      // U_j rows: wrench lane (jr, sr): U[sr][t] = sum_w Bb[sr][w] (W0^-1 Bb')[w][t]
+      {
+        float yv[12];
+        const int hh = jr >= 5 ? 1 : 0, base = 12 * (jr - 5 * hh);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {  // leg g of the step: 3 x 3 block
+          const f4v r0 = S.w0i[hh][base + 3 * g], r1 = S.w0i[hh][base + 3 * g + 1],
+                    r2 = S.w0i[hh][base + 3 * g + 2];
+          const float b0 = S.Bb[sr][3 * g], b1 = S.Bb[sr][3 * g + 1], b2 = S.Bb[sr][3 * g + 2];
+          yv[3 * g + 0] = b0 * r0.x + b1 * r1.x + b2 * r2.x;
+          yv[3 * g + 1] = b0 * r0.y + b1 * r1.y + b2 * r2.y;
+          yv[3 * g + 2] = b0 * r0.z + b1 * r1.z + b2 * r2.z;
+        }
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+          float acc = 0.0f;
+#pragma unroll
+          for (int w = 0; w < 12; ++w) acc = fmaf(yv[w], S.Bb[t][w], acc);
+          if (wvalid) S.U[jr][sr][t] = acc;
+        }
+      }
+      lsync();
+      // per step: L_j (Cholesky of U_j), L_j^-1, rows of Te L_j -- every lane of
+      // the step computes the factor, lane sr writes its row / column
+      float Lcol[6];  // column sr of L_jr
+      {
+        float Um[6][6], L[6][6], Li[6][6];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+          for (int c = 0; c < 6; ++c) Um[r][c] = wvalid ? S.U[jr][r][c] : (r == c ? 1.0f : 0.0f);
+        chol6(Um, L, Li);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          float lsr = 0.0f, lisr = 0.0f, tl = 0.0f;
+#pragma unroll
+          for (int c = 0; c < 6; ++c) {
+            lsr = (c == sr) ? L[r][c] : lsr;
+            lisr = (c == sr) ? Li[r][c] : lisr;
+          }
+          Lcol[r] = lsr;
+          if (lane < 60) {
+            if (r >= sr) {
+              S.Lt[jr][tri(sr) - sr + r] = lsr;   // column sr of L_j
+              S.Li[jr][tri(sr) - sr + r] = lisr;  // column sr of L_j^-1
+            }
+          }
+          (void)tl;
+        }
+        if (lane < 60) {
+          // row sr of Te L_j
+#pragma unroll
+          for (int c = 0; c < 6; ++c) {
+            float tl = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) tl = fmaf(S.Te[sr][r], L[r][c], tl);
+            S.TL[jr][sr][c] = tl;
+          }
+        }
+      }
+      lsync();
+      // S = I + L' (cG) L, this lane's row: S[(jr,sr),(k,t)] = delta + c (K0 alpha.L_k[:,t] + K2 beta.L_k[:,t])
+      {
+        float al[6], be[6];
+#pragma unroll
+        for (int s = 0; s < 6; ++s) al[s] = S.q2[6 + s] * Lcol[s];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+          float acc = 0.0f;
+#pragma unroll
+          for (int s = 0; s < 6; ++s) acc = fmaf(Lcol[s], S.Te[s][t], acc);
+          be[t] = acc;
+        }
+#pragma unroll
+        for (int c = 0; c < 60; ++c) {
+          const int k = c / 6, t = c - 6 * (c / 6);
+          const float *lk = &S.Lt[k][tri(t) - t];  // column t of L_k (uniform): rows t..5
+          float da = 0.0f, db = 0.0f;
+#pragma unroll
+          for (int s = t; s < 6; ++s) {
+            da = fmaf(al[s], lk[s], da);
+            db = fmaf(be[s], lk[s], db);
+          }
+          const f2v kk = S.k0k2[jr][k];
+          float v = csf * fmaf(kk.x, da, kk.y * db);
+          v = wvalid ? v : 0.0f;
+          T.k[c] = v + (c == ln ? 1.0f : 0.0f);
+        }
+#pragma unroll
+        for (int c = 60; c < 64; ++c) T.k[c] = 0.0f;
+      }
+      // S^-1 in place
+      lit_invert(S, lane, nw, T);
+      // Z = S^-1 blockdiag(L_k^-1), this lane's row in place (L_k^-1 lower
+      // triangular: column (k, t) from the columns (k, t' >= t))
+#pragma unroll
+      for (int k = 0; k < kLitN; ++k) {
+        float o[6];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+          const float *li = &S.Li[k][tri(t) - t];  // column t of L_k^-1: rows t..5
+          float acc = 0.0f;
+#pragma unroll
+          for (int tp = t; tp < 6; ++tp) acc = fmaf(T.k[6 * k + tp], li[tp], acc);
+          o[t] = acc;
+        }
+#pragma unroll
+        for (int t = 0; t < 6; ++t) T.k[6 * k + t] = o[t];
+      }
+      // T = cG (L Z), four columns per pass, in place: the step's six rows give
+      // M = L Z and Te M (= (Te L) Z), the horizon sums with K0 / K2 give
+      // (cG M)[(j,s)] = c (Qb_s sum_k K0(j,k) M[(k,s)] + sum_k K2(j,k) (Te M)[(k,s)])
+      {
+        float lrow[6], tlrow[6];  // row sr of L_jr and of Te L_jr
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          const float lv = S.Lt[jr][tri(c) - c + (sr > c ? sr : c)];  // in bounds for every lane
+          lrow[c] = c <= sr ? lv : 0.0f;
+          tlrow[c] = S.TL[jr][sr][c];
+        }
+        const float qb = S.q2[6 + sr];
+#pragma unroll
+        for (int g = 0; g < 15; ++g) {
+          S.zc[lane] = (f4v){T.k[4 * g], T.k[4 * g + 1], T.k[4 * g + 2], T.k[4 * g + 3]};
+          lsync();
+          f4v m = (f4v)(0.0f), tm = (f4v)(0.0f);
+#pragma unroll
+          for (int s2 = 0; s2 < 6; ++s2) {
+            const f4v zr = S.zc[6 * jr + s2];
+            m = __builtin_elementwise_fma((f4v)(lrow[s2]), zr, m);
+            tm = __builtin_elementwise_fma((f4v)(tlrow[s2]), zr, tm);
+          }
+          // L Z overwrites Z: the wave's LDS reads above complete in order first
+          asm volatile("" ::: "memory");
+          S.zc[lane] = m;
+          S.tc[lane] = tm;
+          lsync();
+          f4v o0 = (f4v)(0.0f), o2 = (f4v)(0.0f);
+#pragma unroll
+          for (int k = 0; k < kLitN; ++k) {
+            const f2v kk = S.k0k2[jr][k];
+            o0 = __builtin_elementwise_fma((f4v)(kk.x), S.zc[6 * k + sr], o0);
+            o2 = __builtin_elementwise_fma((f4v)(kk.y), S.tc[6 * k + sr], o2);
+          }
+          const f4v o = (f4v)(csf) * __builtin_elementwise_fma((f4v)(qb), o0, o2);
+          T.k[4 * g + 0] = wvalid ? o.x : 0.0f;
+          T.k[4 * g + 1] = wvalid ? o.y : 0.0f;
+          T.k[4 * g + 2] = wvalid ? o.z : 0.0f;
+          T.k[4 * g + 3] = wvalid ? o.w : 0.0f;
+        }
+        lsync();
+      }
+      // a = W0^-1 D^-1 b and x~ = D^-1 (a - W0^-1 t): per-lane coefficients
+      // from this lane's W0^-1 rows (LDS)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f4v wi = S.w0i[h][lane];
+        const Triple dd = triple(dinv[h], comp);
+        A1[h][0] = valid[h] ? wi.x * dd.v0 : 0.0f;
+        A1[h][1] = valid[h] ? wi.y * dd.v1 : 0.0f;
+        A1[h][2] = valid[h] ? wi.z * dd.v2 : 0.0f;
+        B1[h][0] = valid[h] ? dinv[h] * wi.x : 0.0f;
+        B1[h][1] = valid[h] ? dinv[h] * wi.y : 0.0f;
+        B1[h][2] = valid[h] ? dinv[h] * wi.z : 0.0f;
+      }
+    }
+    bool refactor = false;
+
+    for (;;) {
+      if (iter < a.max_iter) {
+        int next = a.max_iter;
+        if (ctm) next = min(next, (iter / ctm + 1) * ctm);
+        if (interval) next = min(next, (iter / interval + 1) * interval);
+        const float rva[2][2] = {{eq0[0] ? 1e3f * rho : rho, rho}, {eq0[1] ? 1e3f * rho : rho, rho}};
+        const float rvb = 1.0f / rho;
+        const float rvia[2] = {eq0[0] ? 1e-3f * rvb : rvb, eq0[1] ? 1e-3f * rvb : rvb};
+        for (; iter < next; ++iter) {
+          asm volatile("" ::: "memory");
+          // rhs = sigma x - q + A'(rho z - y) per slot, then a = W0^-1 D^-1 rhs
+          float av[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f4v arz = S.arz[h][lane];
+            const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
+            const f2v rv = {rva[h][0], rva[h][1]};
+            const f2v w = __builtin_elementwise_fma(rv, z[h], -y[h]);
+            const f2v aw = ra * w, zw = rz * w;
+            const float tz = zw.x + zw.y;
+            float rhs = fmaf(sigma, x[h], (aw.x + aw.y) - qv[h]);
+            {
+              const float m2 = comp == 2 ? 1.0f : 0.0f;
+              float u;
+              asm("s_nop 1\n\t"
+                  "v_add_f32_dpp %0, %2, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+                  "s_nop 1\n\t"
+                  "v_fmac_f32_dpp %1, %0, %3 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+                  : "=&v"(u), "+v"(rhs)
+                  : "v"(tz), "v"(m2));
+            }
+            const Triple rt = triple(rhs, comp);
+            av[h] = fmaf(A1[h][0], rt.v0, fmaf(A1[h][1], rt.v1, A1[h][2] * rt.v2));
+            S.av[h][lane] = av[h];
+          }
+          lsync();
+          // v = Vu a: wrench row (jr, sr) over its step's 12 variables
+          float wr = 0.0f;
+          {
+            const int hh = jr >= 5 ? 1 : 0, base = 12 * (jr - 5 * hh);
+            const f4v *src = reinterpret_cast<const f4v *>(&S.av[hh][base]);
+            const f4v u0 = src[0], u1 = src[1], u2 = src[2];
+            const float uv[12] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w, u2.x, u2.y, u2.z, u2.w};
+            const f4v *br = reinterpret_cast<const f4v *>(S.Bb[sr]);
+            const f4v b0 = br[0], b1 = br[1], b2 = br[2];
+            const float bv[12] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w};
+            float w0 = 0.0f, w1 = 0.0f;
+#pragma unroll
+            for (int w = 0; w < 12; w += 2) {
+              w0 = fmaf(bv[w], uv[w], w0);
+              w1 = fmaf(bv[w + 1], uv[w + 1], w1);
+            }
+            wr = w0 + w1;
+          }
+          const int buf = iter & 1;
+          reinterpret_cast<float *>(&S.bc[buf][0])[lane] = wr;
+          lsync();
+          // s = T v (DPP broadcast matvec, 60 columns)
+          float sv;
+          {
+            const f4v r0 = S.bc[buf][lane & 15];
+            float acc0, acc1;
+            QL_DPP_MATVEC60_2(acc0, acc1, r0, T.k, 0);
+            sv = acc0 + acc1;
+          }
+          S.wv[lane] = sv;
+          lsync();
+          // x~ = D^-1 a - D^-1 W0^-1 Vu' s, then update_x / update_z / update_y
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const float *gs = &S.wv[6 * step[h]];
+            const f2v s01 = *reinterpret_cast<const f2v *>(gs), s23 = *reinterpret_cast<const f2v *>(gs + 2),
+                      s45 = *reinterpret_cast<const f2v *>(gs + 4);
+            const float sf = comp == 0 ? s23.y : (comp == 1 ? s45.x : s45.y);
+            const float tv = fmaf(bwo[h][0], s01.x, fmaf(bwo[h][1], s01.y, fmaf(bwo[h][2], s23.x, dtm * sf)));
+            const Triple tt = triple(tv, comp);
+            const float xt = fmaf(Dinv[h], av[h],
+                                  -fmaf(B1[h][0], tt.v0, fmaf(B1[h][1], tt.v1, B1[h][2] * tt.v2)));
+            const f4v arz = S.arz[h][lane];
+            const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
+            const f2v bnd = S.zb[h][lane];
+            const float n1 = lane_next(xt), n2 = lane_next(n1);
+            const float xtz = comp == 0 ? n2 : n1;
+            x[h] = fmaf(alpha, xt, oma * x[h]);
+            const f2v rv = {rva[h][0], rva[h][1]};
+            const f2v rvi2 = {rvia[h], rvb};
+            const f2v zt = __builtin_elementwise_fma(rz, (f2v)(xtz), ra * xt);
+            const f2v zr = __builtin_elementwise_fma((f2v)(alpha), zt, oma * z[h]);
+            const f2v v = __builtin_elementwise_fma(y[h], rvi2, zr);
+            const f2v zn = {__builtin_amdgcn_fmed3f(v.x, bnd.x, bnd.y), __builtin_amdgcn_fmed3f(v.y, -INFINITY, 0.0f)};
+            y[h] = __builtin_elementwise_fma(rv, zr - zn, y[h]);
+            z[h] = zn;
+          }
+        }
+      }
+      const bool fin = iter >= a.max_iter;
+      const bool can_check = ctm && iter > 0 && (iter % ctm == 0);
+      const bool do_rho = interval && iter > 0 && (iter % interval == 0);
+      if (!(can_check || do_rho || fin)) continue;
+      float o[6], r[6];
+      residuals(o, r, do_rho);
+      const float pri_res = o[0], dua_res = cinv * o[3];
+      if (can_check) {
+        const float eps_p = a.eps_abs + a.eps_rel * fmaxf(o[1], o[2]);
+        const float eps_d = a.eps_abs + a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
+        if (pri_res < eps_p && dua_res < eps_d) {
+          status = QLOCO_OK;
+          break;
+        }
+      }
+      if (do_rho) {  // compute_rho_estimate + adapt_rho
+        const float pn = r[0] / (fmaxf(r[1], r[2]) + 1e-30f);
+        const float dn = r[3] / (fmaxf(fmaxf(qn[1], r[4]), r[5]) + 1e-30f);
+        float rho_new = rho * sqrtf(pn / (dn + 1e-30f));
+        rho_new = fminf(fmaxf(rho_new, 1e-6f), 1e6f);
+        if (rho_new > rho * a.rho_tol || rho_new < rho / a.rho_tol) {
+          rho = rho_new;
+          rho_updates++;
+          if (!fin) {
+            refactor = true;
+            break;
+          }
+        }
+      }
+      if (fin) {
+        const float ep = 10.f * a.eps_abs + 10.f * a.eps_rel * fmaxf(o[1], o[2]);
+        const float ed = 10.f * a.eps_abs + 10.f * a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
+        status = (pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE : QLOCO_MAX_ITER;
+        break;
+      }
+    }
+    if (!refactor) break;
+  }
+
+  // ---------------- 7. outputs: unscale, objective, leg slots (A1RobotControl.cpp:593-599)
+  float xu[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) xu[h] = valid[h] ? x[h] * Dr[h] : 0.0f;
+  float ob = 0.0f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) ob += valid[h] ? cinv * (0.5f * x[h] * px[h] + qv[h] * x[h]) : 0.0f;
+  const float objp = wsum(ob);
+  const bool bad = !isfinite(objp);
+  if (bad) status = QLOCO_NAN;
+  if (a.u) {
+    float *uo = a.u + b * 12 * N;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (valid[h]) uo[60 * h + lane] = bad ? NAN : xu[h];
+  }
+  // u0: step-0 forces (variables 0..11 = slot 0, lanes 0..11); optional body frame R' u
+  {
+    const float n1 = lane_next(xu[0]), n2 = lane_next(n1);
+    const float p1 = lane_prev(xu[0]), p2 = lane_prev(p1);
+    const float f0 = comp == 0 ? xu[0] : (comp == 1 ? p1 : p2);
+    const float f1 = comp == 0 ? n1 : (comp == 1 ? xu[0] : p1);
+    const float f2 = comp == 0 ? n2 : (comp == 1 ? n1 : xu[0]);
+    if (lane < 12) {
+      float o = xu[0];
+      if (a.output_frame == 1)  // R^T f with R = [[c,s,0],[-s,c,0],[0,0,1]]
+        o = comp == 0 ? (R00 * f0 + R10 * f1) : (comp == 1 ? (R01 * f0 + R11 * f1) : f2);
+      a.u0[b * 12 + lane] = bad ? NAN : o;
+    }
+  }
+  if (prec) {  // the persistent record for the next call (layout QLOCO_SRBD_PERSIST_LEN)
+    for (int k = lane; k < NP + 4; k += 64) prec[k] = 0.0f;
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (!valid[h]) continue;
+      const int vidx = 12 * step[h] + 3 * leg[h] + comp, rbase = 20 * step[h] + 5 * leg[h] + 2 * comp;
+      prec[vidx] = x[h];
+      prec[52 * N + vidx] = xu[h];
+      prec[84 * N + vidx] = q_raw[h];
+      prec[12 * N + rbase] = z[h].x;
+      prec[32 * N + rbase] = y[h].x;
+      const f2v e = row_e(h);
+      prec[64 * N + rbase] = cinv * e.x * y[h].x;
+      if (xy) {
+        prec[12 * N + rbase + 1] = z[h].y;
+        prec[32 * N + rbase + 1] = y[h].y;
+        prec[64 * N + rbase + 1] = cinv * e.y * y[h].y;
+      }
+    }
+    for (int k = lane; k < 4 * N; k += 64) prec[96 * N + k] = S.ctf[k];
+    if (lane == 0) {
+      prec[NP] = rho;
+      prec[NP + 1] = 1.0f;
+    }
+  }
+  if (WS && a.warm_start == 1) {
+    const int nu = 12 * N, ncn = 20 * N;
+    float *wx = a.warm + b * (nu + ncn);
+    float *wy = wx + nu;
+    for (int k = lane; k < nu + ncn; k += 64) wx[k] = 0.0f;
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (!valid[h]) continue;
+      wx[12 * step[h] + 3 * leg[h] + comp] = xu[h];
+      const int rbase = 20 * step[h] + 5 * leg[h] + 2 * comp;
+      const f2v e = row_e(h);
+      wy[rbase] = cinv * e.x * y[h].x;
+      if (xy) wy[rbase + 1] = cinv * e.y * y[h].y;
+    }
+  }
+  if (lane == 0) {
+    if (a.status) a.status[b] = status;
+    if (a.iters) a.iters[b] = iter;
+    if (a.rho_updates) a.rho_updates[b] = rho_updates;
+    if (a.obj) a.obj[b] = objp;
+  }
+}
+
+template <bool WS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLitWpe)))
+void srbd_lit_kernel(const SrbdArgs a) {
+  __shared__ __attribute__((aligned(16))) LitLds S;
+  const int64_t i = blockIdx.x;
+  if (i >= a.batch) return;
+  srbd_lit_one<WS>(a, S, i);
+}
+
+int srbd_lit_launch(const SrbdArgs &a, bool warm, hipStream_t stream) {
+  const dim3 grid((unsigned)a.batch);
+  if (warm)
+    hipLaunchKernelGGL(srbd_lit_kernel<true>, grid, dim3(64), 0, stream, a);
+  else
+    hipLaunchKernelGGL(srbd_lit_kernel<false>, grid, dim3(64), 0, stream, a);
+  QLOCO_HIP_CHECK(hipGetLastError(), "srbd_lit_kernel launch");
+  return QLOCO_OK;
+}
+
+}  // namespace qloco

@@ -5,6 +5,7 @@
 # stops the call on the first failure (no GPU step after a failed one).
 # Steps:
 #   tests        pytest -m gpu (parity suite)            -> pytest_gpu.log
+#   tk=EXPR      pytest -m gpu -k EXPR                   -> pytest_k.log
 #   smoke        __graft_entry__.smoke()                 -> smoke.log
 #   bench        python bench.py (default line)          -> bench.json
 #   ktrace       rocprofv3 --kernel-trace --stats of the bench -> kernel_stats.csv
@@ -40,6 +41,10 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
         > "$out/pytest_gpu.log" 2>&1 || fail "$out/pytest_gpu.log"
       tail -n 1 "$out/pytest_gpu.log" ;;
+    tk)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${arg//:/ }" \
+        > "$out/pytest_k.log" 2>&1 || fail "$out/pytest_k.log"
+      tail -n 1 "$out/pytest_k.log" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 \
         || fail "$out/smoke.log"
