@@ -435,29 +435,32 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int w = 0; w < 12; ++w) asm volatile("" : "+v"(bet[h][w]), "+v"(eps[h][w]));
-      float m0 = 0.0f, m1 = 0.0f;
+      // both slots' rows as fp32 pairs (v_pk_fma / v_pk_mul), two max chains each
+      f2v ma = (f2v)(0.0f), mb = (f2v)(0.0f);
 #pragma unroll
       for (int kc = 0; kc < kLitN; ++kc) {
         asm volatile("" ::: "memory");  // table reads stay in the pass (no LICM)
         __builtin_amdgcn_sched_barrier(0);
         const f2v k0 = S.k0k2[step[0]][kc], k1 = S.k0k2[step[1]][kc];
+        const f2v kx = {k0.x, k1.x}, ky = {k0.y, k1.y};
         const f4v *dc = reinterpret_cast<const f4v *>(&S.dcol[12 * kc]);
         const f4v da = scaled ? dc[0] : (f4v)(1.0f), db = scaled ? dc[1] : (f4v)(1.0f),
                   dd = scaled ? dc[2] : (f4v)(1.0f);
         const float dv[12] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w, dd.x, dd.y, dd.z, dd.w};
 #pragma unroll
         for (int w = 0; w < 12; ++w) {
-          const float p0 = fmaf(k0.y, eps[0][w], k0.x * bet[0][w]);
-          const float p1 = fmaf(k1.y, eps[1][w], k1.x * bet[1][w]);
-          m0 = fmaxf(m0, fabsf(p0) * dv[w]);
-          m1 = fmaxf(m1, fabsf(p1) * dv[w]);
+          const f2v be = {bet[0][w], bet[1][w]}, ep = {eps[0][w], eps[1][w]};
+          const f2v p = __builtin_elementwise_fma(ky, ep, kx * be) * (f2v)(dv[w]);
+          f2v &acc = (w & 1) ? mb : ma;
+          acc.x = fmaxf(acc.x, fabsf(p.x));
+          acc.y = fmaxf(acc.y, fabsf(p.y));
         }
         // pin the step's arithmetic here (no sinking into a late masked block
         // that would keep every step's loads live)
-        asm volatile("" : "+v"(m0), "+v"(m1));
+        asm volatile("" : "+v"(ma), "+v"(mb));
       }
-      m[0] = valid[0] ? m0 : 0.0f;
-      m[1] = valid[1] ? m1 : 0.0f;
+      m[0] = valid[0] ? fmaxf(ma.x, mb.x) : 0.0f;
+      m[1] = valid[1] ? fmaxf(ma.y, mb.y) : 0.0f;
     };
     float cnP[2];
     {
@@ -802,6 +805,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       }
       lsync();
       // S = I + L' (cG) L, this lane's row: S[(jr,sr),(k,t)] = delta + c (K0 alpha.L_k[:,t] + K2 beta.L_k[:,t])
+      float cS;  // c sS (the scaling below)
       {
         float al[6], be[6];
 #pragma unroll
@@ -813,6 +817,24 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
           for (int s = 0; s < 6; ++s) acc = fmaf(Lcol[s], S.Te[s][t], acc);
           be[t] = acc;
         }
+        // S is built scaled by sS = 1 / max_r S[r][r]: the pivots of a Gauss-
+        // Jordan on an SPD matrix never exceed its largest diagonal entry, and
+        // the fused pivot-row update (A - A (1 - 1/p)) loses eps * p relative
+        // accuracy -- at small rho S reaches 1e4 and ADMM diverged (DESIGN.md
+        // §3i).  T = cG L S^-1 L^-1 = (c sS) G L (sS S)^-1 L^-1.
+        float sS;
+        {
+          float da = 0.0f, db = 0.0f;  // this lane's own column: L_jr[:, sr] = Lcol
+#pragma unroll
+          for (int s = 0; s < 6; ++s) {
+            da = fmaf(al[s], Lcol[s], da);
+            db = fmaf(be[s], Lcol[s], db);
+          }
+          const f2v kk = S.k0k2[jr][jr];
+          const float dg = wvalid ? 1.0f + csf * fmaf(kk.x, da, kk.y * db) : 1.0f;
+          sS = 1.0f / wmax_nonneg(dg);
+        }
+        cS = csf * sS;
 #pragma unroll
         for (int c = 0; c < 60; ++c) {
           const int k = c / 6, t = c - 6 * (c / 6);
@@ -824,9 +846,9 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
             db = fmaf(be[s], lk[s], db);
           }
           const f2v kk = S.k0k2[jr][k];
-          float v = csf * fmaf(kk.x, da, kk.y * db);
+          float v = cS * fmaf(kk.x, da, kk.y * db);
           v = wvalid ? v : 0.0f;
-          T.k[c] = v + (c == ln ? 1.0f : 0.0f);
+          T.k[c] = v + (c == ln ? sS : 0.0f);
         }
 #pragma unroll
         for (int c = 60; c < 64; ++c) T.k[c] = 0.0f;
@@ -884,7 +906,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
             o0 = __builtin_elementwise_fma((f4v)(kk.x), S.zc[6 * k + sr], o0);
             o2 = __builtin_elementwise_fma((f4v)(kk.y), S.tc[6 * k + sr], o2);
           }
-          const f4v o = (f4v)(csf) * __builtin_elementwise_fma((f4v)(qb), o0, o2);
+          const f4v o = (f4v)(cS) * __builtin_elementwise_fma((f4v)(qb), o0, o2);
           T.k[4 * g + 0] = wvalid ? o.x : 0.0f;
           T.k[4 * g + 1] = wvalid ? o.y : 0.0f;
           T.k[4 * g + 2] = wvalid ? o.z : 0.0f;
@@ -916,6 +938,9 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         const float rva[2][2] = {{eq0[0] ? 1e3f * rho : rho, rho}, {eq0[1] ? 1e3f * rho : rho, rho}};
         const float rvb = 1.0f / rho;
         const float rvia[2] = {eq0[0] ? 1e-3f * rvb : rvb, eq0[1] ? 1e-3f * rvb : rvb};
+        // wave-uniform trip count (a scalar loop, not an exec-masked one)
+        iter = __builtin_amdgcn_readfirstlane(iter);
+        next = __builtin_amdgcn_readfirstlane(next);
         for (; iter < next; ++iter) {
           asm volatile("" ::: "memory");
           // rhs = sigma x - q + A'(rho z - y) per slot, then a = W0^-1 D^-1 rhs
@@ -979,8 +1004,9 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const float *gs = &S.wv[6 * step[h]];
-            const f2v s01 = *reinterpret_cast<const f2v *>(gs), s23 = *reinterpret_cast<const f2v *>(gs + 2),
-                      s45 = *reinterpret_cast<const f2v *>(gs + 4);
+            const f2v s01 = *reinterpret_cast<const f2v *>(gs), s23 = *reinterpret_cast<const f2v *>(gs + 2);
+            f2v s45 = *reinterpret_cast<const f2v *>(gs + 4);
+            asm volatile("" : "+v"(s45));  // loaded by every lane (no exec-masked load)
             const float sf = comp == 0 ? s23.y : (comp == 1 ? s45.x : s45.y);
             const float tv = fmaf(bwo[h][0], s01.x, fmaf(bwo[h][1], s01.y, fmaf(bwo[h][2], s23.x, dtm * sf)));
             const Triple tt = triple(tv, comp);
