@@ -75,6 +75,31 @@ def srbd_flops_executed(n, iters, rho_updates, horizon, checks):
     return build + fac + iters + chk
 
 
+def srbd_flops_executed_lit(horizon, iters, rho_updates, checks):
+    """Useful FP32 flops of the one-wave literal kernel (N <= 10):
+    n = 12N variables, w = 6N wrench rows.  Ruiz: 11 sweeps of the n x n P
+    row norms (4 flops an entry); per (re)factorisation the W0 leg blocks,
+    U_j, the per-step Cholesky, the S rows (17 flops an entry), the 2 w^3
+    Gauss-Jordan, Z = S^-1 L^-1 and T = cG L Z (66 flops an entry); per
+    iteration the T matvec (2 w^2) and the leg / wrench-row work."""
+    N = float(horizon)
+    n, w = 12.0 * N, 6.0 * N
+    it = np.asarray(iters, dtype=np.float64)
+    ru = np.asarray(rho_updates, dtype=np.float64)
+    ch = np.asarray(checks, dtype=np.float64)
+    build = 11.0 * n * n * 4.0 + 2 * 13 * N * 13 + 2 * 13 * N * n + 144 * 6 * 4
+    fac = (1.0 + ru) * (2.0 * w ** 3 + w * w * (17.0 + 66.0) + 40.0 * n + 144.0 * w + 600.0 * N + 420.0 * w)
+    its = it * (2.0 * w * w + 30.0 * n + 24.0 * w)
+    chk = ch * (40.0 * n + 40.0 * w)
+    return build + fac + its + chk
+
+
+def executed_flops(N, n_var, iters, rho_up, checks, literal):
+    if literal and N <= 10:
+        return srbd_flops_executed_lit(N, iters, rho_up, checks)
+    return srbd_flops_executed(n_var, iters, rho_up, N, checks)
+
+
 def _config_tag(N, gait, B):
     """Which BASELINE.json config a bench line measures (per-GPU share for the
     8-GPU configs: 524288/8 = 65536, 1048576/8 = 131072)."""
@@ -352,7 +377,7 @@ def main():
     n_var = 12 * N * np.ones(B) if args.literal else 3 * ct.reshape(B, -1).sum(axis=1)
     checks = iters // 25 + iters // 100
     flops_alg = float(srbd_flops_alg(N, iters, rho_up).sum())
-    flops_exec = float(srbd_flops_executed(n_var, iters, rho_up, N, checks).sum())
+    flops_exec = float(executed_flops(N, n_var, iters, rho_up, checks, args.literal).sum())
     achieved_tflops = flops_alg / (kern_ms.mean() * 1e-3) / 1e12
     executed_tflops = flops_exec / (kern_ms.mean() * 1e-3) / 1e12
 
@@ -409,7 +434,7 @@ def main():
                                      ", which the stance-only kernel never builds", flops_exec)),
         },
     }
-    tfile = os.path.join(ROOT, "profiles", "traffic_srbd_n%d_b%d.json" % (N, B))
+    tfile = os.path.join(ROOT, "profiles", "traffic_srbd_n%d_b%d%s.json" % (N, B, "_lit" if args.literal else ""))
     if os.path.exists(tfile):
         with open(tfile) as f:
             res["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
@@ -451,7 +476,7 @@ def literal_line(args, srbd, d_x0, d_xr, d_ft, d_ct, stream, dev):
     status = out.status.cpu().numpy()
     checks = iters // 25 + iters // 100
     fa = float(srbd_flops_alg(N, iters, rho_up).sum())
-    fe = float(srbd_flops_executed(12 * N * np.ones(B), iters, rho_up, N, checks).sum())
+    fe = float(executed_flops(N, 12 * N * np.ones(B), iters, rho_up, checks, True).sum())
     kt = float(per.mean()) * 1e-3
     return {"value": round(B * K / elapsed, 1), "unit": "solves/s", "steps": K,
             "ms_per_step": round(elapsed / K * 1e3, 4),
@@ -464,7 +489,8 @@ def literal_line(args, srbd, d_x0, d_xr, d_ft, d_ct, stream, dev):
             "note": "the reference's call as written (A1RobotControl.cpp:557-578): all 12N "
                     "forces ADMM variables, swing legs held by fz in [0, 0] equality rows; "
                     "%d variables per N = %d instance -> %s" % (
-                        12 * N, N, "two-wavefront workgroups" if 4 * N <= 42
+                        12 * N, N, "one wavefront, the OSQP solve through the per-step wrench "
+                        "space (srbd_lit_kernel, DESIGN.md 3i)" if N <= 10
                         else "512-thread workgroups (srbd_admm_big_kernel)")}
 
 
