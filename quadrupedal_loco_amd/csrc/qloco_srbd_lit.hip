@@ -124,26 +124,38 @@ __device__ __forceinline__ Triple triple(float v, int comp) {
 }
 
 // In-place Gauss-Jordan inverse of the 60 x 60 SPD S (one row per lane,
-// eigenvalues >= 1): invert_w1's scheme on the literal LDS.
+// pivots <= 1 after the 1/max-diagonal scaling): invert_w1's scheme (DESIGN.md
+// §3) with one pivot of look-ahead -- pivot k first applies its update to
+// column k + 1 alone (the same fused multiply-add the full update performs,
+// so bit-identical) and publishes pivot k + 1's broadcast row, then runs the
+// other 59 columns while that LDS write is in flight.
 __device__ __forceinline__ void lit_invert(LitLds &S, int lane, int ncol, Row<1> &K) {
   int nc = __builtin_amdgcn_readfirstlane(ncol);
-#pragma unroll
-  for (int k = 0; k < 60; ++k) {
+  {
+    const float v = K.k[0];
+    const float p = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+    reinterpret_cast<float *>(&S.bc[0][0])[lane] = lane == 0 ? p + 1.0f : v;
+  }
+  ColLoop<0, 60>::run([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
     asm volatile("" : "+s"(nc));
-    if (k >= nc) continue;
-    float *bcf = reinterpret_cast<float *>(&S.bc[k & 1][0]);
+    if (k >= nc) return;
     int tt = lane;
     asm volatile("" : "+v"(tt));
-    const float v = K.k[k];
-    const float p = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
-    bcf[tt] = (tt == k) ? p + 1.0f : ((tt < k) ? -v : v);
     lsync();
     const f4v r0 = S.bc[k & 1][lane & 15];
+    const float v = K.k[k];
+    const float p = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
     const float pinv = __builtin_amdgcn_rcpf(p);
     const float ng = -((tt == k) ? (1.0f - pinv) : v * pinv);
+    if constexpr (k + 1 < 60) {  // unconditional (harmless past the last pivot): no branch to join
+      const float la = fmaf(dpp_col<k + 1>(r0), ng, K.k[k + 1]);
+      const float p1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, la), k + 1));
+      reinterpret_cast<float *>(&S.bc[(k + 1) & 1][0])[tt] = (tt == k + 1) ? p1 + 1.0f : ((tt < k + 1) ? -la : la);
+    }
     QL_DPP_GJ60(K.k, 0, r0, ng);
     if (p > kGjExactPivot) K.k[k] = (tt == k) ? pinv : ng;
-  }
+  });
   lsync();
 }
 
@@ -435,17 +447,24 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int w = 0; w < 12; ++w) asm volatile("" : "+v"(bet[h][w]), "+v"(eps[h][w]));
-      // both slots' rows as fp32 pairs (v_pk_fma / v_pk_mul), two max chains each
+      // both slots' rows as fp32 pairs (v_pk_fma / v_pk_mul), two max chains
+      // each; the next column step's LDS reads are issued before this step's
+      // arithmetic (one step of look-ahead, no more: all ten would be live)
       f2v ma = (f2v)(0.0f), mb = (f2v)(0.0f);
+      const f4v one4 = (f4v)(1.0f);
+      f2v k0 = S.k0k2[step[0]][0], k1 = S.k0k2[step[1]][0];
+      f4v da = scaled ? reinterpret_cast<const f4v *>(&S.dcol[0])[0] : one4,
+          db = scaled ? reinterpret_cast<const f4v *>(&S.dcol[0])[1] : one4,
+          dd = scaled ? reinterpret_cast<const f4v *>(&S.dcol[0])[2] : one4;
 #pragma unroll
       for (int kc = 0; kc < kLitN; ++kc) {
+        const int kn = kc + 1 < kLitN ? kc + 1 : kc;
         asm volatile("" ::: "memory");  // table reads stay in the pass (no LICM)
+        const f2v k0n = S.k0k2[step[0]][kn], k1n = S.k0k2[step[1]][kn];
+        const f4v *dcn = reinterpret_cast<const f4v *>(&S.dcol[12 * kn]);
+        const f4v dan = scaled ? dcn[0] : one4, dbn = scaled ? dcn[1] : one4, ddn = scaled ? dcn[2] : one4;
         __builtin_amdgcn_sched_barrier(0);
-        const f2v k0 = S.k0k2[step[0]][kc], k1 = S.k0k2[step[1]][kc];
         const f2v kx = {k0.x, k1.x}, ky = {k0.y, k1.y};
-        const f4v *dc = reinterpret_cast<const f4v *>(&S.dcol[12 * kc]);
-        const f4v da = scaled ? dc[0] : (f4v)(1.0f), db = scaled ? dc[1] : (f4v)(1.0f),
-                  dd = scaled ? dc[2] : (f4v)(1.0f);
         const float dv[12] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w, dd.x, dd.y, dd.z, dd.w};
 #pragma unroll
         for (int w = 0; w < 12; ++w) {
@@ -458,6 +477,12 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         // pin the step's arithmetic here (no sinking into a late masked block
         // that would keep every step's loads live)
         asm volatile("" : "+v"(ma), "+v"(mb));
+        __builtin_amdgcn_sched_barrier(0);
+        k0 = k0n;
+        k1 = k1n;
+        da = dan;
+        db = dbn;
+        dd = ddn;
       }
       m[0] = valid[0] ? fmaxf(ma.x, mb.x) : 0.0f;
       m[1] = valid[1] ? fmaxf(ma.y, mb.y) : 0.0f;
