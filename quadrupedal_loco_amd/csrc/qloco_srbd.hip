@@ -440,29 +440,39 @@ __device__ __forceinline__ void invert_w1(SrbdLds<1, NM> &S, int t, int ncol, Ro
   int nc = __builtin_amdgcn_readfirstlane(ncol);
   // pivots emitted: 60 when the one-wave class stops at 20 legs (code size)
   constexpr int KP = (C60 && kW1Legs <= 20) ? 60 : 64;
-#pragma unroll
-  for (int k = 0; k < KP; ++k) {
+  // one pivot of look-ahead: pivot k applies its update to column k + 1 first
+  // (the same fused multiply-add the full update performs: bit-identical) and
+  // publishes pivot k + 1's row, which is in flight during the other columns
+  {
+    const float v = K.k[0];
+    const float p = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+    reinterpret_cast<float *>(&S.bc[0][0])[lane] = lane == 0 ? p + 1.0f : v;
+  }
+  ColLoop<0, KP>::run([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
     asm volatile("" : "+s"(nc));  // the per-pivot compare stays a scalar one (not 64 hoisted masks)
-    if (k >= nc) continue;  // wave-uniform; the loop stays fully unrolled (static register k)
-    const int buf = k & 1;
-    float *bcf = reinterpret_cast<float *>(&S.bc[buf][0]);
+    if (k >= nc) return;  // wave-uniform (static register k: the pivot loop is unrolled)
     int tt = t;
     asm volatile("" : "+v"(tt));  // per-pivot compares stay local (no 64 hoisted masks)
+    bsync<1>();
+    const f4v r0 = S.bc[k & 1][lane & 15];
     const float v = K.k[k];
     const float p = __builtin_bit_cast(
         float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
-    bcf[tt] = (tt == k) ? p + 1.0f : ((tt < k) ? -v : v);
-    bsync<1>();
-    const f4v r0 = S.bc[buf][lane & 15];
     const float pinv = __builtin_amdgcn_rcpf(p);
     const float ng = -((tt == k) ? (1.0f - pinv) : v * pinv);
+    if constexpr (k + 1 < KP) {  // unconditional past the last pivot (harmless): no branch to join
+      const float la = fmaf(dpp_col<k + 1>(r0), ng, K.k[k + 1]);
+      const float p1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, la), k + 1));
+      reinterpret_cast<float *>(&S.bc[(k + 1) & 1][0])[tt] = (tt == k + 1) ? p1 + 1.0f : ((tt < k + 1) ? -la : la);
+    }
     if constexpr (C60) {
       QL_DPP_GJ60(K.k, 0, r0, ng);
     } else {
       QL_DPP_GJ64(K.k, 0, r0, ng);
     }
     if (p > kGjExactPivot) K.k[k] = (tt == k) ? pinv : ng;  // column k exactly
-  }
+  });
   bsync<1>();
 }
 

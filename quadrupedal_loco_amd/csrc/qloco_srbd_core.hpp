@@ -4,6 +4,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "qloco_common.hpp"
 #include "qloco_dpp.inc"
 
@@ -53,6 +55,30 @@ __device__ __forceinline__ float dpp(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF,
                                                             0xF, false));
 }
+// Compile-time loop over columns C..E-1 (the DPP control of a column's
+// broadcast must be a constant expression).
+template <int C, int E>
+struct ColLoop {
+  template <class F>
+  static __device__ __forceinline__ void run(F &&f) {
+    f(std::integral_constant<int, C>{});
+    ColLoop<C + 1, E>::run(f);
+  }
+};
+template <int E>
+struct ColLoop<E, E> {
+  template <class F>
+  static __device__ __forceinline__ void run(F &&) {}
+};
+// Column c of a 60-vector read as one 16-byte chunk per lane (lane l holds
+// elements 4(l % 16) .. +3): DPP row_newbcast:(c / 4) of component c % 4.
+template <int C>
+__device__ __forceinline__ float dpp_col(const f4v &d) {
+  constexpr int e = C & 3;
+  const float v = e == 0 ? d.x : (e == 1 ? d.y : (e == 2 ? d.z : d.w));
+  return dpp<0x150 + (C >> 2)>(v);
+}
+
 __device__ __forceinline__ float lane_prev(float v) { return dpp<0x138>(v); }  // wave_shr:1
 __device__ __forceinline__ float lane_next(float v) { return dpp<0x130>(v); }  // wave_shl:1
 __device__ __forceinline__ float rlane(float v, int l) {

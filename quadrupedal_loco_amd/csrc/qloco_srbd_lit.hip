@@ -73,30 +73,6 @@ struct LitLds {
 };
 static_assert(sizeof(LitLds) <= 13653, "literal kernel: three workgroups per SIMD need <= 160 KB / 12 of LDS");
 
-// Compile-time loop over columns C..E-1 (the DPP control of a column's
-// broadcast must be a constant expression).
-template <int C, int E>
-struct ColLoop {
-  template <class F>
-  static __device__ __forceinline__ void run(F &&f) {
-    f(std::integral_constant<int, C>{});
-    ColLoop<C + 1, E>::run(f);
-  }
-};
-template <int E>
-struct ColLoop<E, E> {
-  template <class F>
-  static __device__ __forceinline__ void run(F &&) {}
-};
-// Column c of a 60-vector read as one 16-byte chunk per lane (lane l holds
-// elements 4(l % 16) .. +3): DPP row_newbcast:(c / 4) of component c % 4.
-template <int C>
-__device__ __forceinline__ float dpp_col(const f4v &d) {
-  constexpr int e = C & 3;
-  const float v = e == 0 ? d.x : (e == 1 ? d.y : (e == 2 ? d.z : d.w));
-  return dpp<0x150 + (C >> 2)>(v);
-}
-
 // Packed lower-triangular 6 x 6 columns: column t (rows t..5) starts at
 // tri(t); tri(t) - t + s addresses row s >= t.
 __device__ __forceinline__ constexpr int tri(int t) { return 6 * t - (t * (t - 1)) / 2; }
@@ -640,7 +616,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       if (valid[h]) {
         const float *gs = &S.wv[6 * step[h]];
         acc = bwo[h][0] * gs[0] + bwo[h][1] * gs[1] + bwo[h][2] * gs[2] + dtm * gs[3 + comp];
-        acc = fmaf(r2v[h], x[h] * Dr[h], acc);
+        acc = fmaf(S.r2[3 * leg[h] + comp], x[h] * Dr[h], acc);  // valid slot: r2 of its leg
       }
       out[h] = cs * Dr[h] * acc;
     }
@@ -747,7 +723,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         const Triple dd = triple(dinv[h], comp);
         // W0 row = D^-1 M D^-1 + c R (diagonal)
         float w0 = dinv[h] * m0 * dd.v0, w1 = dinv[h] * m1 * dd.v1, w2 = dinv[h] * m2 * dd.v2;
-        const float cr = csf * r2v[h];
+        const float cr = csf * (valid[h] ? S.r2[3 * leg[h] + comp] : 0.0f);
         w0 += comp == 0 ? cr : 0.0f;
         w1 += comp == 1 ? cr : 0.0f;
         w2 += comp == 2 ? cr : 0.0f;
@@ -1118,8 +1094,10 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     const float f2 = comp == 0 ? n2 : (comp == 1 ? n1 : xu[0]);
     if (lane < 12) {
       float o = xu[0];
-      if (a.output_frame == 1)  // R^T f with R = [[c,s,0],[-s,c,0],[0,0,1]]
-        o = comp == 0 ? (R00 * f0 + R10 * f1) : (comp == 1 ? (R01 * f0 + R11 * f1) : f2);
+      if (a.output_frame == 1) {  // R^T f with R = [[c,s,0],[-s,c,0],[0,0,1]], recomputed here
+        const float yw = S.x0[2], cw = cosf(yw), sw = sinf(yw);
+        o = comp == 0 ? (cw * f0 - sw * f1) : (comp == 1 ? (sw * f0 + cw * f1) : f2);
+      }
       a.u0[b * 12 + lane] = bad ? NAN : o;
     }
   }

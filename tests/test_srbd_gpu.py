@@ -713,11 +713,12 @@ def test_srbd_literal_rho_interval_matches_restatement(interval):
 
 
 @pytest.mark.parametrize("N,B,gait,samples", [(10, 4096, "trot", 16), (16, 65536, "trot", 8),
-                                              (20, 65536, "pace", 6)])
+                                              (20, 65536, "pace", 6), (10, 131072, "mixed", 8)])
 def test_srbd_literal_full_size_sampled(N, B, gait, samples):
     """The literal QP at full size, one launch each: BASELINE configs[1]
-    (N = 10 trot, 4096) and the per-GPU shares of configs[2] / [3] (N = 16
-    trot, N = 20 pace: 65,536 each; the wide 512-thread kernel).  Whole
+    (N = 10 trot, 4096) and the per-GPU shares of configs[2] / [3] / [4]
+    (N = 16 trot, N = 20 pace: 65,536 each, the wide 512-thread kernel;
+    N = 10 mixed: 131,072, the one-wave wrench-space kernel).  Whole
     batch: every instance converges, forces finite and inside the friction
     pyramid, swing forces within the ADMM tolerance of zero, u0 = u[:12], and
     a second launch is bit-identical.  Instances spread over the batch (both

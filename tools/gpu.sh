@@ -84,7 +84,7 @@ for step in "$@"; do
       done
       cat "$out/configs.jsonl" ;;
     lit)
-      for spec in "10 trot 4096" "16 trot 8192" "20 pace 8192"; do
+      for spec in "10 trot 4096" "10 mixed 131072" "16 trot 8192" "20 pace 8192"; do
         set -- $spec
         N=$1 GAIT=$2 LITERAL=1 timeout -k 10 120 python tools/perf_kernel.py default $3 10 >> "$out/literal.txt" 2>&1 \
           || fail "$out/literal.txt"
