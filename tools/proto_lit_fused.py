@@ -1,0 +1,95 @@
+"""The literal kernel's fused Gauss-Jordan in float32 (numpy emulation):
+with and without the 1/max-diagonal scaling of S, against the fp64
+restatement at fixed rho -- a derivation check, not
+product code.
+
+    python tools/proto_lit_fused.py [id ...]
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tests"))
+sys.path.insert(0, os.path.dirname(HERE))
+import proto_lit as P  # noqa: E402
+import oracle_lib as O  # noqa: E402
+from srbd_ref import Instance  # noqa: E402
+
+from quadrupedal_loco_amd import srbd  # noqa: E402
+
+f = np.float32
+
+
+def gj_fused(S, exact=16.0):
+    """In-place symmetric Gauss-Jordan as the kernel runs it: broadcast row
+    (pivot + 1 on the diagonal, sign-flipped processed columns), one fused
+    multiply-add per entry, the exact pivot column above `exact`."""
+    A = S.astype(f).copy()
+    n = A.shape[0]
+    idx = np.arange(n)
+    for k in range(n):
+        v = A[:, k].copy()
+        p = A[k, k]
+        bc = np.where(idx == k, f(p + f(1)), np.where(idx < k, -v, v)).astype(f)
+        pinv = f(1) / p
+        ng = np.where(idx == k, -(f(1) - pinv), -(v * pinv)).astype(f)
+        A = (A.astype(np.float64) + np.outer(ng.astype(np.float64), bc.astype(np.float64))).astype(f)
+        if p > exact:
+            A[:, k] = np.where(idx == k, pinv, ng)
+    return A
+
+
+def solver(scaled):
+    class Fused(P.WrenchSolve):
+        def __init__(self, G, Vu, D, E, c, sigma, Araw, rho_vec, Rdiag, f32):
+            super().__init__(G, Vu, D, E, c, sigma, Araw, rho_vec, Rdiag, True)
+            N6, n = G.shape[0], Vu.shape[1]
+            AE = Araw * E[:, None]
+            W0 = (np.diag(c * Rdiag + sigma / D ** 2) + AE.T @ (rho_vec[:, None] * AE)).astype(f)
+            W0i = np.zeros_like(W0)
+            for b in range(n // 3):
+                sl = slice(3 * b, 3 * b + 3)
+                W0i[sl, sl] = np.linalg.inv(W0[sl, sl])
+            Vu32 = Vu.astype(f)
+            U = (Vu32 @ W0i @ Vu32.T).astype(f)
+            L = np.zeros_like(U)
+            Li = np.zeros_like(U)
+            for j in range(N6 // 6):
+                sl = slice(6 * j, 6 * j + 6)
+                L[sl, sl] = np.linalg.cholesky(U[sl, sl])
+                Li[sl, sl] = np.linalg.inv(L[sl, sl])
+            Gc = (c * G).astype(f)
+            S = (np.eye(N6, dtype=f) + L.T @ Gc @ L).astype(f)
+            s = f(1.0 / np.diag(S).max()) if scaled else f(1)
+            Si = (gj_fused((S * s).astype(f)) * s).astype(f)
+            self.T = (Gc @ (L @ (Si @ Li).astype(f)).astype(f)).astype(f)
+    return Fused
+
+
+def main():
+    N = 10
+    ids = [int(a) for a in sys.argv[1:]] or [2647, 1]
+    x0, xr, ft, ct = srbd.generate(20261015, N, max(ids) + 1, "trot")
+    sp = O.srbd_spec(N=N)
+    base = P.WrenchSolve
+    for b in ids:
+        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
+        G, Vu = P.wrench_model(x0[b], ft[b], N)
+        for rho in (1e-2, 1e-3, 3e-4, 1e-4):
+            st = dict(rho=rho, sigma=1e-6, alpha=1.6, eps_abs=1e-3, eps_rel=1e-3, ctm=25, tol=1e30)
+            xo, info = inst.admm_full(rho=rho, adaptive_rho=0, max_iter=600)
+            out = ["b=%d rho %.0e restatement it %d st %d" % (b, rho, info.iters, info.status)]
+            for scaled in (False, True):
+                P.WrenchSolve = solver(scaled)
+                xm, it, stt, _, _ = P.admm(inst, G, Vu, "wrench32", st=st, max_iter=600)
+                P.WrenchSolve = base
+                out.append("fused%s it %d st %d |du| %.3g" % ("+scaled" if scaled else "", it, stt,
+                                                              np.abs(xm - xo).max()))
+            print("  ".join(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
