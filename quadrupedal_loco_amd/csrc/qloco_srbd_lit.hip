@@ -99,6 +99,37 @@ __device__ __forceinline__ Triple triple(float v, int comp) {
   return t;
 }
 
+// A leg-triple dot product sum_j a_j v(leg, j) as lane shifts d = j - comp:
+// v(l + d) with coefficient c_d (zero where l + d leaves the leg), five fused
+// multiply-adds with DPP operands instead of the triple's 4 moves + 6 selects
+// + 3 multiply-adds.
+struct Shift5 {
+  float cm2, cm1, c0, cp1, cp2;
+};
+__device__ __forceinline__ Shift5 shift5(float a0, float a1, float a2, int comp) {
+  Shift5 c;
+  c.c0 = comp == 0 ? a0 : (comp == 1 ? a1 : a2);
+  c.cm1 = comp == 1 ? a0 : (comp == 2 ? a1 : 0.0f);
+  c.cm2 = comp == 2 ? a0 : 0.0f;
+  c.cp1 = comp == 0 ? a1 : (comp == 1 ? a2 : 0.0f);
+  c.cp2 = comp == 0 ? a2 : 0.0f;
+  return c;
+}
+__device__ __forceinline__ float tdot(float v, const Shift5 &c) {
+  float a, t, u;
+  asm("s_nop 1\n\t"
+      "v_mov_b32_dpp %1, %3 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+      "v_mov_b32_dpp %2, %3 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+      "v_mul_f32 %0, %3, %4\n\t"
+      "v_fmac_f32_dpp %0, %3, %5 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+      "v_fmac_f32_dpp %0, %3, %7 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+      "v_fmac_f32_dpp %0, %1, %6 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+      "v_fmac_f32_dpp %0, %2, %8 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+      : "=&v"(a), "=&v"(t), "=&v"(u)
+      : "v"(v), "v"(c.c0), "v"(c.cm1), "v"(c.cm2), "v"(c.cp1), "v"(c.cp2));
+  return a;
+}
+
 // In-place Gauss-Jordan inverse of the 60 x 60 SPD S (one row per lane,
 // pivots <= 1 after the 1/max-diagonal scaling): invert_w1's scheme (DESIGN.md
 // §3) with one pivot of look-ahead -- pivot k first applies its update to
@@ -560,7 +591,8 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   int status = QLOCO_MAX_ITER, iter = 0, rho_updates = 0;
   float px[2] = {0.0f, 0.0f};
   Row<1> T;        // T = (I + cG U)^-1 cG, this lane's wrench row
-  float A1[2][3], B1[2][3], Dinv[2];
+  Shift5 A1[2], B1[2];  // per slot: rows of W0^-1 D^-1 and D^-1 W0^-1 as leg-triple shifts
+  float Dinv[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) Dinv[h] = valid[h] ? 1.0f / Dr[h] : 0.0f;
 
@@ -921,12 +953,10 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       for (int h = 0; h < 2; ++h) {
         const f4v wi = S.w0i[h][lane];
         const Triple dd = triple(dinv[h], comp);
-        A1[h][0] = valid[h] ? wi.x * dd.v0 : 0.0f;
-        A1[h][1] = valid[h] ? wi.y * dd.v1 : 0.0f;
-        A1[h][2] = valid[h] ? wi.z * dd.v2 : 0.0f;
-        B1[h][0] = valid[h] ? dinv[h] * wi.x : 0.0f;
-        B1[h][1] = valid[h] ? dinv[h] * wi.y : 0.0f;
-        B1[h][2] = valid[h] ? dinv[h] * wi.z : 0.0f;
+        A1[h] = shift5(valid[h] ? wi.x * dd.v0 : 0.0f, valid[h] ? wi.y * dd.v1 : 0.0f,
+                       valid[h] ? wi.z * dd.v2 : 0.0f, comp);
+        B1[h] = shift5(valid[h] ? dinv[h] * wi.x : 0.0f, valid[h] ? dinv[h] * wi.y : 0.0f,
+                       valid[h] ? dinv[h] * wi.z : 0.0f, comp);
       }
     }
     bool refactor = false;
@@ -965,8 +995,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
                   : "=&v"(u), "+v"(rhs)
                   : "v"(tz), "v"(m2));
             }
-            const Triple rt = triple(rhs, comp);
-            av[h] = fmaf(A1[h][0], rt.v0, fmaf(A1[h][1], rt.v1, A1[h][2] * rt.v2));
+            av[h] = tdot(rhs, A1[h]);
             S.av[h][lane] = av[h];
           }
           lsync();
@@ -1010,9 +1039,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
             asm volatile("" : "+v"(s45));  // loaded by every lane (no exec-masked load)
             const float sf = comp == 0 ? s23.y : (comp == 1 ? s45.x : s45.y);
             const float tv = fmaf(bwo[h][0], s01.x, fmaf(bwo[h][1], s01.y, fmaf(bwo[h][2], s23.x, dtm * sf)));
-            const Triple tt = triple(tv, comp);
-            const float xt = fmaf(Dinv[h], av[h],
-                                  -fmaf(B1[h][0], tt.v0, fmaf(B1[h][1], tt.v1, B1[h][2] * tt.v2)));
+            const float xt = fmaf(Dinv[h], av[h], -tdot(tv, B1[h]));
             const f4v arz = S.arz[h][lane];
             const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
             const f2v bnd = S.zb[h][lane];
