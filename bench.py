@@ -11,13 +11,16 @@ instance range is regenerated locally from (seed, global id)) and the solved
 contact forces are all-gathered over RCCL/xGMI inside the timed step.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-                    [--horizon 10] [--gait trot] [--no-cpu-baseline] [--literal]
+                    [--horizon 10] [--gait trot] [--no-cpu-baseline] [--reduced]
 
-The headline solves the stance-only reduction of each QP (swing forces
-eliminated exactly: same optimum).  At N=1 the same line also
-carries `literal_full_qp`: the same workload solved as the reference's
-literal 12N-variable QP (spec.literal_full_qp = 1), timed in
-the same run; `--literal` makes the literal form the headline.
+The headline solves the reference's call as written: the literal
+12N-variable QP, every force an ADMM variable and the swing legs held by
+their fz in [0, 0] rows (spec.literal_full_qp = 1, A1RobotControl.cpp:557-578;
+N <= 10 on one wavefront through the wrench space).  At N=1
+the same line also carries `reduced_qp`: the same workload solved as the
+stance-only reduction (swing forces eliminated exactly: same optimum,
+different ADMM iterates), timed in the same run; `--reduced`
+makes the reduction the headline (then the second line is `literal_full_qp`).
 
 Rank 0 prints ONE JSON line.  Launch for N>1 GPUs:
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -201,11 +204,14 @@ def main():
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--gait", default="trot")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--reduced", action="store_true",
+                    help="headline = the stance-only reduction (literal_full_qp = 0) instead of "
+                         "the reference's literal 12N-variable QP")
     ap.add_argument("--literal", action="store_true",
-                    help="headline = the reference's literal 12N-variable QP (literal_full_qp = 1)")
-    ap.add_argument("--no-literal-line", action="store_true",
-                    help="skip the literal-QP side measurement at N = 1")
-    ap.add_argument("--literal-steps", type=int, default=50)
+                    help="the literal QP as headline (the default; kept for old command lines)")
+    ap.add_argument("--no-literal-line", "--no-second-line", dest="no_second_line",
+                    action="store_true", help="skip the other formulation's side measurement at N = 1")
+    ap.add_argument("--literal-steps", "--second-steps", dest="second_steps", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (0: every usable host core)")
@@ -225,6 +231,7 @@ def main():
     ap.add_argument("--dist-selftest", action="store_true",
                     help="testing (CPU): launch path + gloo all-gather only, no GPU")
     args = ap.parse_args()
+    args.literal = not args.reduced
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
 
@@ -439,8 +446,9 @@ def main():
         with open(tfile) as f:
             res["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
 
-    if rank == 0 and world == 1 and not args.literal and not args.no_literal_line:
-        res["literal_full_qp"] = literal_line(args, srbd, d_x0, d_xr, d_ft, d_ct, stream, dev)
+    if rank == 0 and world == 1 and not args.no_second_line:
+        key = "reduced_qp" if args.literal else "literal_full_qp"
+        res[key] = second_line(args, srbd, d_x0, d_xr, d_ft, d_ct, ct, stream, dev, not args.literal)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(N, args.gait, args.cpu_seconds, args.cpu_threads)
     if rank == 0:
@@ -451,22 +459,24 @@ def main():
         dist.destroy_process_group()
 
 
-def literal_line(args, srbd, d_x0, d_xr, d_ft, d_ct, stream, dev):
-    """The same workload solved as the reference's literal 12N-variable QP
-    (literal_full_qp = 1: swing forces kept as ADMM variables), timed after the
-    headline loop: barrier-free single-GPU timing, HIP events per launch."""
+def second_line(args, srbd, d_x0, d_xr, d_ft, d_ct, ct, stream, dev, literal):
+    """The same workload in the other formulation -- the reference's literal
+    12N-variable QP (literal_full_qp = 1: swing forces kept as ADMM variables)
+    or the stance-only reduction -- timed after the headline loop:
+    barrier-free single-GPU timing, HIP events per launch."""
     import torch
-    B, N, K = args.batch, args.horizon, args.literal_steps
-    solver = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=1)
+    B, N, K = args.batch, args.horizon, args.second_steps
+    solver = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=int(literal))
+    legs = 4 * N if literal else srbd.max_stance_legs(ct, N)
     out = solver.alloc_outputs(B, dev)
     for _ in range(5):
-        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, stream=stream.cuda_stream)
+        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, max_legs=legs, stream=stream.cuda_stream)
     torch.cuda.synchronize(dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1)]
     t0 = time.perf_counter()
     ev[0].record(stream)
     for i in range(K):
-        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, stream=stream.cuda_stream)
+        solver.solve(d_x0, d_xr, d_ft, d_ct, out=out, max_legs=legs, stream=stream.cuda_stream)
         ev[i + 1].record(stream)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -476,7 +486,8 @@ def literal_line(args, srbd, d_x0, d_xr, d_ft, d_ct, stream, dev):
     status = out.status.cpu().numpy()
     checks = iters // 25 + iters // 100
     fa = float(srbd_flops_alg(N, iters, rho_up).sum())
-    fe = float(executed_flops(N, 12 * N * np.ones(B), iters, rho_up, checks, True).sum())
+    n_var = 12 * N * np.ones(B) if literal else 3 * ct.reshape(B, -1).sum(axis=1)
+    fe = float(executed_flops(N, n_var, iters, rho_up, checks, literal).sum())
     kt = float(per.mean()) * 1e-3
     return {"value": round(B * K / elapsed, 1), "unit": "solves/s", "steps": K,
             "ms_per_step": round(elapsed / K * 1e3, 4),
@@ -486,12 +497,15 @@ def literal_line(args, srbd, d_x0, d_xr, d_ft, d_ct, stream, dev):
             "status_ok_frac": float(np.mean(status == 0)),
             "frac": round(fa / kt / 1e12 / PEAK_FP32_TFLOPS, 4),
             "executed_frac": round(fe / kt / 1e12 / PEAK_FP32_TFLOPS, 4),
-            "note": "the reference's call as written (A1RobotControl.cpp:557-578): all 12N "
-                    "forces ADMM variables, swing legs held by fz in [0, 0] equality rows; "
-                    "%d variables per N = %d instance -> %s" % (
-                        12 * N, N, "one wavefront, the OSQP solve through the per-step wrench "
-                        "space (srbd_lit_kernel, DESIGN.md 3i)" if N <= 10
-                        else "512-thread workgroups (srbd_admm_big_kernel)")}
+            "note": ("the reference's call as written (A1RobotControl.cpp:557-578): all 12N "
+                     "forces ADMM variables, swing legs held by fz in [0, 0] equality rows; "
+                     "%d variables per N = %d instance -> %s" % (
+                         12 * N, N, "one wavefront, the OSQP solve through the per-step wrench "
+                         "space (srbd_lit_kernel, DESIGN.md 3i)" if N <= 10
+                         else "512-thread workgroups (srbd_admm_big_kernel)")) if literal else
+                    "stance-only reduction of the same QPs (swing forces eliminated exactly: "
+                    "same optimum, different ADMM iterates and Ruiz scaling; DESIGN.md 3): "
+                    "closed-form P rows, K^-1 in registers, one wavefront for <= 20 stance legs"}
 
 
 def cpu_baseline(N, gait, seconds, threads):
