@@ -36,20 +36,21 @@
 
 namespace qloco {
 
-constexpr int kLitWpe = 3;  // waves per SIMD: 168 VGPRs, <= 13.3 KB of LDS (static_assert below)
+constexpr int kLitWpe = 4;  // waves per SIMD: 128 VGPRs, <= 10 KB of LDS (static_assert below)
 
 struct LitLds {
-  f4v bc[2][16];            // broadcast ring: 60-vectors read as one 16-B chunk per lane
+  f4v bc[16];               // broadcast row: 60-vectors read as one 16-B chunk per lane (one
+                            // wave: its LDS ops run in order, so one buffer serves every reuse)
   float av[2][64];          // per-slot exchange (a, D x, t)
   float wv[64];             // wrench rows (s, w)
-  float tw[64];             // wrench rows (Te w)
   f2v k0k2[kLitN][kLitN];   // horizon sums K0 / K2 (row step, column step)
   float Bb[6][12];          // wrench map (constant feet), rows omega 0..2, v 3..5
   float Te[6][6];           // dt^2 blockdiag(Rz' Qtheta Rz, Qp)
   float q2[16], r2[12], x0[16];
   float ctf[4 * kLitN];     // contact flags as floats
-  f2v zb[2][64];            // per slot: scaled bounds of row 0 (row 1: [-inf, 0])
   f4v arz[2][64];           // per slot: scaled A entries (ra0, ra1, rz0, rz1)
+  float zh[2][64];          // per slot: row 0's scaled upper bound (x / y rows: inf); the lower
+                            // bound is 0 (x / y) or zh fz_min / fz_max (z rows)
   union {                   // phase-local storage (LDS bounds the occupancy: <= 20 KB)
     struct {                // gradient + Ruiz
       f2v beps[12][12];     // (beta, eps)[w][w']: the P entries' per-column coefficients
@@ -58,12 +59,13 @@ struct LitLds {
       float Wc[12 * kLitN];
     };
     struct {                // factorisation
-      f4v w0i[2][64];       // per variable: its row of W0^-1 (x, y, z) + pad
-      float TL[kLitN][6][6];  // per step: rows of Te L_j
       float Lt[kLitN][21];    // per step: columns of L_j, packed (column t: rows t..5 at tri(t))
       float Li[kLitN][21];    // per step: columns of L_j^-1, packed the same way
       union {
-        float U[kLitN][6][6];  // per step: U_j (until its Cholesky)
+        struct {
+          float w0i[3][2][64];     // per variable: its row of W0^-1 (x, y, z), until the U rows
+          float U[kLitN][6][6];    // per step: U_j (until its Cholesky)
+        };
         struct {
           f4v zc[64], tc[64];  // T passes: Z (then L Z, same wave, in order), Te L Z columns
         };
@@ -71,7 +73,7 @@ struct LitLds {
     };
   };
 };
-static_assert(sizeof(LitLds) <= 13653, "literal kernel: three workgroups per SIMD need <= 160 KB / 12 of LDS");
+static_assert(sizeof(LitLds) <= 10240, "literal kernel: four workgroups per SIMD need <= 160 KB / 16 of LDS");
 
 // Packed lower-triangular 6 x 6 columns: column t (rows t..5) starts at
 // tri(t); tri(t) - t + s addresses row s >= t.
@@ -141,7 +143,7 @@ __device__ __forceinline__ void lit_invert(LitLds &S, int lane, int ncol, Row<1>
   {
     const float v = K.k[0];
     const float p = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
-    reinterpret_cast<float *>(&S.bc[0][0])[lane] = lane == 0 ? p + 1.0f : v;
+    reinterpret_cast<float *>(&S.bc[0])[lane] = lane == 0 ? p + 1.0f : v;
   }
   ColLoop<0, 60>::run([&](auto kc) {
     constexpr int k = decltype(kc)::value;
@@ -150,7 +152,7 @@ __device__ __forceinline__ void lit_invert(LitLds &S, int lane, int ncol, Row<1>
     int tt = lane;
     asm volatile("" : "+v"(tt));
     lsync();
-    const f4v r0 = S.bc[k & 1][lane & 15];
+    const f4v r0 = S.bc[lane & 15];
     const float v = K.k[k];
     const float p = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
     const float pinv = __builtin_amdgcn_rcpf(p);
@@ -158,7 +160,7 @@ __device__ __forceinline__ void lit_invert(LitLds &S, int lane, int ncol, Row<1>
     if constexpr (k + 1 < 60) {  // unconditional (harmless past the last pivot): no branch to join
       const float la = fmaf(dpp_col<k + 1>(r0), ng, K.k[k + 1]);
       const float p1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, la), k + 1));
-      reinterpret_cast<float *>(&S.bc[(k + 1) & 1][0])[tt] = (tt == k + 1) ? p1 + 1.0f : ((tt < k + 1) ? -la : la);
+      reinterpret_cast<float *>(&S.bc[0])[tt] = (tt == k + 1) ? p1 + 1.0f : ((tt < k + 1) ? -la : la);
     }
     QL_DPP_GJ60(K.k, 0, r0, ng);
     if (p > kGjExactPivot) K.k[k] = (tt == k) ? pinv : ng;
@@ -367,13 +369,6 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   }
   // from here on a variable's B_d column is all the iterations need of lo/hi:
   // its omega rows (the wrench map's torque part; the force part is dtm e_comp)
-  float bwo[2][3];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    bwo[h][0] = lo[h].x;
-    bwo[h][1] = lo[h].y;
-    bwo[h][2] = lo[h].z;
-  }
   // persistent solver (warm_start == 2): literal semantics -- after the
   // first call every call takes OSQP's update path
   const int NP = 100 * N;
@@ -553,7 +548,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   for (int h = 0; h < 2; ++h) {
     const float lh0 = rl0[h] * rE0[h], uh0 = ru0[h] * rE0[h];
     eq0[h] = valid[h] && !xy && (uh0 - lh0 < 1e-4f);  // OSQP set_rho_vec: RHO_TOL
-    S.zb[h][lane] = (f2v){lh0, uh0};
+    S.zh[h][lane] = uh0;
     S.arz[h][lane] = (f4v){ra0[h], ra1[h], rz0[h], rz1[h]};
     qn[0] = fmaxf(qn[0], valid[h] ? fabsf(qv[h] / Dr[h]) : 0.0f);
     qn[1] = fmaxf(qn[1], valid[h] ? fabsf(qv[h]) : 0.0f);
@@ -591,7 +586,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   int status = QLOCO_MAX_ITER, iter = 0, rho_updates = 0;
   float px[2] = {0.0f, 0.0f};
   Row<1> T;        // T = (I + cG U)^-1 cG, this lane's wrench row
-  Shift5 A1[2], B1[2];  // per slot: rows of W0^-1 D^-1 and D^-1 W0^-1 as leg-triple shifts
+  Shift5 W1[2];  // per slot: this lane's row of W0^-1 as leg-triple shifts
   float Dinv[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) Dinv[h] = valid[h] ? 1.0f / Dr[h] : 0.0f;
@@ -622,7 +617,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       float tw = 0.0f;
 #pragma unroll
       for (int t = 0; t < 6; ++t) tw = fmaf(S.Te[sr][t], S.wv[6 * jr + t], tw);
-      S.tw[lane] = wvalid ? tw : 0.0f;
+      reinterpret_cast<float *>(&S.bc[0])[lane] = wvalid ? tw : 0.0f;  // Te w (bc is free in a check)
     }
     lsync();
     // (G w)[(jr, sr)] = Qb_s sum_k K0(jr,k) w(k,sr) + sum_k K2(jr,k) (Te w_k)_sr
@@ -634,7 +629,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       for (int k = 0; k < kLitN; ++k) {
         const f2v kk = S.k0k2[jr][k];
         s0 = fmaf(kk.x, S.wv[6 * k + sr], s0);
-        s2 = fmaf(kk.y, S.tw[6 * k + sr], s2);
+        s2 = fmaf(kk.y, reinterpret_cast<const float *>(&S.bc[0])[6 * k + sr], s2);
       }
       gw = wvalid ? fmaf(qb, s0, s2) : 0.0f;
     }
@@ -647,7 +642,8 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       float acc = 0.0f;
       if (valid[h]) {
         const float *gs = &S.wv[6 * step[h]];
-        acc = bwo[h][0] * gs[0] + bwo[h][1] * gs[1] + bwo[h][2] * gs[2] + dtm * gs[3 + comp];
+        const int wc = lane % 12;  // the variable's column of Bb (both slots: 60 = 5 x 12)
+        acc = S.Bb[0][wc] * gs[0] + S.Bb[1][wc] * gs[1] + S.Bb[2][wc] * gs[2] + dtm * gs[3 + comp];
         acc = fmaf(S.r2[3 * leg[h] + comp], x[h] * Dr[h], acc);  // valid slot: r2 of its leg
       }
       out[h] = cs * Dr[h] * acc;
@@ -734,9 +730,10 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       int ln = lane;
       float csf = cs, dinv[2] = {Dinv[0], Dinv[1]};
       asm volatile("" : "+v"(ln), "+v"(csf), "+v"(dinv[0]), "+v"(dinv[1]));
-      // W0 rows (D-unscaled leg blocks) and their inverses, per slot
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      // this lane's row of W0^-1 for slot h (W0 = D^-1 (sigma I + A~' rho A~) D^-1 +
+      // c R, 3 x 3 per leg): written for the U rows, recomputed for the
+      // iteration coefficients after the T phase (its LDS is the T passes')
+      auto w0_inv_row = [&](int h, float &i0, float &i1, float &i2) {
         const f4v arz = S.arz[h][lane];
         const float rv0 = eq0[h] ? 1e3f * rho : rho, rv1 = rho;
         const float d_own = rv0 * arz.x * arz.x + rv1 * arz.y * arz.y;
@@ -770,10 +767,17 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         const float k10 = a12 * a20 - a10 * a22, k11 = a00 * a22 - a02 * a20, k12 = a02 * a10 - a00 * a12;
         const float k20 = a10 * a21 - a11 * a20, k21 = a01 * a20 - a00 * a21, k22 = a00 * a11 - a01 * a10;
         const float idet = 1.0f / (a00 * k00 + a01 * k10 + a02 * k20);
-        const float i0 = (comp == 0 ? k00 : (comp == 1 ? k10 : k20)) * idet;  // row comp of W0^-1
-        const float i1 = (comp == 0 ? k01 : (comp == 1 ? k11 : k21)) * idet;
-        const float i2 = (comp == 0 ? k02 : (comp == 1 ? k12 : k22)) * idet;
-        S.w0i[h][lane] = (f4v){i0, i1, i2, 0.0f};
+        i0 = (comp == 0 ? k00 : (comp == 1 ? k10 : k20)) * idet;  // row comp of W0^-1
+        i1 = (comp == 0 ? k01 : (comp == 1 ? k11 : k21)) * idet;
+        i2 = (comp == 0 ? k02 : (comp == 1 ? k12 : k22)) * idet;
+      };
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float i0, i1, i2;
+        w0_inv_row(h, i0, i1, i2);
+        S.w0i[0][h][lane] = i0;
+        S.w0i[1][h][lane] = i1;
+        S.w0i[2][h][lane] = i2;
       }
       lsync();
       // U_j rows: wrench lane (jr, sr): U[sr][t] = sum_w Bb[sr][w] (W0^-1 Bb')[w][t]
@@ -782,8 +786,10 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         const int hh = jr >= 5 ? 1 : 0, base = 12 * (jr - 5 * hh);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {  // leg g of the step: 3 x 3 block
-          const f4v r0 = S.w0i[hh][base + 3 * g], r1 = S.w0i[hh][base + 3 * g + 1],
-                    r2 = S.w0i[hh][base + 3 * g + 2];
+          const int v0 = base + 3 * g;
+          const f4v r0 = {S.w0i[0][hh][v0], S.w0i[1][hh][v0], S.w0i[2][hh][v0], 0.0f},
+                    r1 = {S.w0i[0][hh][v0 + 1], S.w0i[1][hh][v0 + 1], S.w0i[2][hh][v0 + 1], 0.0f},
+                    r2 = {S.w0i[0][hh][v0 + 2], S.w0i[1][hh][v0 + 2], S.w0i[2][hh][v0 + 2], 0.0f};
           const float b0 = S.Bb[sr][3 * g], b1 = S.Bb[sr][3 * g + 1], b2 = S.Bb[sr][3 * g + 2];
           yv[3 * g + 0] = b0 * r0.x + b1 * r1.x + b2 * r2.x;
           yv[3 * g + 1] = b0 * r0.y + b1 * r1.y + b2 * r2.y;
@@ -810,7 +816,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         chol6(Um, L, Li);
 #pragma unroll
         for (int r = 0; r < 6; ++r) {
-          float lsr = 0.0f, lisr = 0.0f, tl = 0.0f;
+          float lsr = 0.0f, lisr = 0.0f;
 #pragma unroll
           for (int c = 0; c < 6; ++c) {
             lsr = (c == sr) ? L[r][c] : lsr;
@@ -822,17 +828,6 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
               S.Lt[jr][tri(sr) - sr + r] = lsr;   // column sr of L_j
               S.Li[jr][tri(sr) - sr + r] = lisr;  // column sr of L_j^-1
             }
-          }
-          (void)tl;
-        }
-        if (lane < 60) {
-          // row sr of Te L_j
-#pragma unroll
-          for (int c = 0; c < 6; ++c) {
-            float tl = 0.0f;
-#pragma unroll
-            for (int r = 0; r < 6; ++r) tl = fmaf(S.Te[sr][r], L[r][c], tl);
-            S.TL[jr][sr][c] = tl;
           }
         }
       }
@@ -908,12 +903,15 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       // M = L Z and Te M (= (Te L) Z), the horizon sums with K0 / K2 give
       // (cG M)[(j,s)] = c (Qb_s sum_k K0(j,k) M[(k,s)] + sum_k K2(j,k) (Te M)[(k,s)])
       {
-        float lrow[6], tlrow[6];  // row sr of L_jr and of Te L_jr
+        float lrow[6], tlrow[6];  // row sr of L_jr and of Te L_jr (Te L from the packed columns)
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
           const float lv = S.Lt[jr][tri(c) - c + (sr > c ? sr : c)];  // in bounds for every lane
           lrow[c] = c <= sr ? lv : 0.0f;
-          tlrow[c] = S.TL[jr][sr][c];
+          float tl = 0.0f;
+#pragma unroll
+          for (int r = c; r < 6; ++r) tl = fmaf(S.Te[sr][r], S.Lt[jr][tri(c) - c + r], tl);
+          tlrow[c] = tl;
         }
         const float qb = S.q2[6 + sr];
 #pragma unroll
@@ -947,16 +945,14 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         }
         lsync();
       }
-      // a = W0^-1 D^-1 b and x~ = D^-1 (a - W0^-1 t): per-lane coefficients
-      // from this lane's W0^-1 rows (LDS)
+      // a = W0^-1 D^-1 b and x~ = D^-1 (a - W0^-1 t): this lane's row of W0^-1
+      // as leg-triple shifts (D^-1 applied elementwise around the two dots)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const f4v wi = S.w0i[h][lane];
-        const Triple dd = triple(dinv[h], comp);
-        A1[h] = shift5(valid[h] ? wi.x * dd.v0 : 0.0f, valid[h] ? wi.y * dd.v1 : 0.0f,
-                       valid[h] ? wi.z * dd.v2 : 0.0f, comp);
-        B1[h] = shift5(valid[h] ? dinv[h] * wi.x : 0.0f, valid[h] ? dinv[h] * wi.y : 0.0f,
-                       valid[h] ? dinv[h] * wi.z : 0.0f, comp);
+        float wx, wy, wz;
+        w0_inv_row(h, wx, wy, wz);
+        const f4v wi = {wx, wy, wz, 0.0f};
+        W1[h] = shift5(valid[h] ? wi.x : 0.0f, valid[h] ? wi.y : 0.0f, valid[h] ? wi.z : 0.0f, comp);
       }
     }
     bool refactor = false;
@@ -966,14 +962,20 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         int next = a.max_iter;
         if (ctm) next = min(next, (iter / ctm + 1) * ctm);
         if (interval) next = min(next, (iter / interval + 1) * interval);
-        const float rva[2][2] = {{eq0[0] ? 1e3f * rho : rho, rho}, {eq0[1] ? 1e3f * rho : rho, rho}};
-        const float rvb = 1.0f / rho;
-        const float rvia[2] = {eq0[0] ? 1e-3f * rvb : rvb, eq0[1] ? 1e-3f * rvb : rvb};
+        const float rho_s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rho)));
+        const float rvb_s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, 1.0f / rho)));
+        const float zlo = a.fz_max > 0.0f ? a.fz_min / a.fz_max : 0.0f;  // z rows: lower = zlo upper
         // wave-uniform trip count (a scalar loop, not an exec-masked one)
         iter = __builtin_amdgcn_readfirstlane(iter);
         next = __builtin_amdgcn_readfirstlane(next);
         for (; iter < next; ++iter) {
           asm volatile("" ::: "memory");
+          // rho vector (eq rows 1e3 rho) from the scalar rho each iteration: per-lane
+          // selects instead of six loop-invariant registers
+          float rr = rho_s, rvb = rvb_s;
+          asm volatile("" : "+v"(rr), "+v"(rvb));
+          const float rva[2][2] = {{eq0[0] ? 1e3f * rr : rr, rr}, {eq0[1] ? 1e3f * rr : rr, rr}};
+          const float rvia[2] = {eq0[0] ? 1e-3f * rvb : rvb, eq0[1] ? 1e-3f * rvb : rvb};
           // rhs = sigma x - q + A'(rho z - y) per slot, then a = W0^-1 D^-1 rhs
           float av[2];
 #pragma unroll
@@ -995,7 +997,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
                   : "=&v"(u), "+v"(rhs)
                   : "v"(tz), "v"(m2));
             }
-            av[h] = tdot(rhs, A1[h]);
+            av[h] = tdot(Dinv[h] * rhs, W1[h]);  // W0^-1 D^-1 rhs
             S.av[h][lane] = av[h];
           }
           lsync();
@@ -1017,20 +1019,22 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
             }
             wr = w0 + w1;
           }
-          const int buf = iter & 1;
-          reinterpret_cast<float *>(&S.bc[buf][0])[lane] = wr;
+          reinterpret_cast<float *>(&S.bc[0])[lane] = wr;
           lsync();
           // s = T v (DPP broadcast matvec, 60 columns)
           float sv;
           {
-            const f4v r0 = S.bc[buf][lane & 15];
+            const f4v r0 = S.bc[lane & 15];
             float acc0, acc1;
             QL_DPP_MATVEC60_2(acc0, acc1, r0, T.k, 0);
             sv = acc0 + acc1;
           }
           S.wv[lane] = sv;
           lsync();
-          // x~ = D^-1 a - D^-1 W0^-1 Vu' s, then update_x / update_z / update_y
+          // x~ = D^-1 a - D^-1 W0^-1 Vu' s, then update_x / update_z / update_y; the
+          // variable's omega rows of B_d from LDS (a padding slot's are harmless:
+          // its leg's B1 coefficients are zero)
+          const float bw0 = S.Bb[0][lane % 12], bw1 = S.Bb[1][lane % 12], bw2 = S.Bb[2][lane % 12];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const float *gs = &S.wv[6 * step[h]];
@@ -1038,11 +1042,12 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
             f2v s45 = *reinterpret_cast<const f2v *>(gs + 4);
             asm volatile("" : "+v"(s45));  // loaded by every lane (no exec-masked load)
             const float sf = comp == 0 ? s23.y : (comp == 1 ? s45.x : s45.y);
-            const float tv = fmaf(bwo[h][0], s01.x, fmaf(bwo[h][1], s01.y, fmaf(bwo[h][2], s23.x, dtm * sf)));
-            const float xt = fmaf(Dinv[h], av[h], -tdot(tv, B1[h]));
+            const float tv = fmaf(bw0, s01.x, fmaf(bw1, s01.y, fmaf(bw2, s23.x, dtm * sf)));
+            const float xt = Dinv[h] * (av[h] - tdot(tv, W1[h]));  // D^-1 (a - W0^-1 t)
             const f4v arz = S.arz[h][lane];
             const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
-            const f2v bnd = S.zb[h][lane];
+            const float hi = S.zh[h][lane];
+            const f2v bnd = {xy ? 0.0f : zlo * hi, hi};
             const float n1 = lane_next(xt), n2 = lane_next(n1);
             const float xtz = comp == 0 ? n2 : n1;
             x[h] = fmaf(alpha, xt, oma * x[h]);
