@@ -204,6 +204,19 @@ __device__ __forceinline__ void chol6(const float (&a)[6][6], float (&L)[6][6], 
   }
 }
 
+// Lane-derived indices re-derived from an opaque copy of the lane at the top
+// of a phase: the address arithmetic on them is then recomputed there (a few
+// VALU) instead of hoisted to the kernel entry and kept live -- at 128 VGPRs
+// the hoisted offsets were the setup's scratch spills.
+#define QL_LIT_LANE_INDICES(LX)                                                                    \
+  int LX = threadIdx.x;                                                                            \
+  asm volatile("" : "+v"(LX));                                                                     \
+  const int jr = LX < 60 ? LX / 6 : kLitN - 1, sr = LX < 60 ? LX - 6 * (LX / 6) : 0;               \
+  const bool wvalid = LX < nw;                                                                     \
+  const int step[2] = {LX < 60 && LX < nvar ? LX / 12 : 0, LX < 60 && 60 + LX < nvar ? (60 + LX) / 12 : 0}; \
+  const int leg[2] = {LX < 60 && LX < nvar ? (LX % 12) / 3 : 0, LX < 60 && 60 + LX < nvar ? ((60 + LX) % 12) / 3 : 0}; \
+  (void)jr; (void)sr; (void)wvalid; (void)step; (void)leg
+
 // WS: a warm-start mode (1 or 2) may be set (the persistent record of
 // DESIGN.md §3c, literal semantics: the update path on every call).
 template <bool WS>
@@ -593,6 +606,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
 
   // P~ x (scaled) per slot: c D (Vu' G Vu + R) D x through the wrench rows
   auto p_times_x = [&](float (&out)[2]) {
+    QL_LIT_LANE_INDICES(lxp);
 #pragma unroll
     for (int h = 0; h < 2; ++h) S.av[h][lane] = valid[h] ? x[h] * Dr[h] : 0.0f;
     lsync();
@@ -730,6 +744,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       int ln = lane;
       float csf = cs, dinv[2] = {Dinv[0], Dinv[1]};
       asm volatile("" : "+v"(ln), "+v"(csf), "+v"(dinv[0]), "+v"(dinv[1]));
+      QL_LIT_LANE_INDICES(lxf);
       // this lane's row of W0^-1 for slot h (W0 = D^-1 (sigma I + A~' rho A~) D^-1 +
       // c R, 3 x 3 per leg): written for the U rows, recomputed for the
       // iteration coefficients after the T phase (its LDS is the T passes')
@@ -965,6 +980,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         const float rho_s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rho)));
         const float rvb_s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, 1.0f / rho)));
         const float zlo = a.fz_max > 0.0f ? a.fz_min / a.fz_max : 0.0f;  // z rows: lower = zlo upper
+        QL_LIT_LANE_INDICES(lxi);
         // wave-uniform trip count (a scalar loop, not an exec-masked one)
         iter = __builtin_amdgcn_readfirstlane(iter);
         next = __builtin_amdgcn_readfirstlane(next);
