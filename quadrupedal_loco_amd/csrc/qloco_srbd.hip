@@ -90,6 +90,7 @@ struct SrbdLds {
   int cst[NC];              // per var: step, NM on padding (row of zeros in k0k2)
   f2v k0k2[NM * (NM + 1)];  // [row step][col step]: horizon sums K0, K2
   float piv[2];
+  float qn[2];              // ||D^-1 q||_inf, ||q||_inf (scaled): read at the checks
   float colv[W == 1 ? 1 : 2][W == 1 ? 1 : NC];  // W = 2 inverse: pivot column
   float red[W][16];
   int legtab[4 * NM];   // stance pair -> 4*step + leg
@@ -170,7 +171,7 @@ __device__ __forceinline__ float bqp_t(const SrbdLds<W, NM> &S, int step, int co
 //      (W0), (i-j) on e rows (W1).
 template <int W, int NM>
 __device__ __forceinline__ void row_scans(SrbdLds<W, NM> &S, int N, bool forward) {
-  const int r = threadIdx.x;
+  const int r = opaque_tid();
   if (r >= 12) return;
   const bool brow = r >= 6;
   float v[NM];
@@ -210,7 +211,7 @@ template <int W, int NB, int NM>
 __device__ __forceinline__ void horizon_rows(SrbdLds<W, NM> &S, int N) {
   constexpr int NT = 64 * W;
   if constexpr (NB == 0) {  // any horizon: rolled loops (cold configurations)
-    for (int idx = threadIdx.x; idx < 12 * N; idx += NT) {
+    for (int idx = opaque_tid(); idx < 12 * N; idx += NT) {
       const int j = idx / 12, r = idx - 12 * j;
       const f2v *kr = &S.k0k2[j * (NM + 1)];
       float acc = 0.0f;
@@ -221,7 +222,7 @@ __device__ __forceinline__ void horizon_rows(SrbdLds<W, NM> &S, int N) {
   }
 #pragma unroll
   for (int pass = 0; pass < (12 * (NB > 0 ? NB : 1) + NT - 1) / NT; ++pass) {
-    const int idx = threadIdx.x + NT * pass;
+    const int idx = opaque_tid() + NT * pass;
     if (idx < 12 * N) {
       const int j = idx / 12, r = idx - 12 * j;
       const f2v *kr = &S.k0k2[j * (NM + 1)];
@@ -254,7 +255,7 @@ template <int W, int NM>
 __device__ __forceinline__ float p_times_x(SrbdLds<W, NM> &S, int N, bool valid, int step, int comp,
                                            f4v lo, f4v hi, float r2v, float xu, float dtm,
                                            float dt2m) {
-  const int t = threadIdx.x;
+  const int t = opaque_tid();
   for (int idx = t; idx < 12 * N; idx += 64 * W) {
     const int j = idx / 12, s = idx - 12 * j;
     const int sg = s / 3, sc = s - 3 * sg;  // 0: e rows, 1: p rows, 2: b rows, 3: v rows
@@ -631,15 +632,18 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       for (int k = t; k < 4 * N; k += 64 * W) mism |= (prec[96 * N + k] != 0.0f) != (S.ct[k] != 0);
     p_same = p_init && !__syncthreads_or(mism);
   }
-  int ncol[W];
+  // valid columns per wave, from the stance-leg count (re-read from LDS at
+  // each factorisation rather than kept live across the ADMM loop)
+  auto col_counts = [&](int nl, int (&ncol)[W]) {
 #pragma unroll
-  for (int w = 0; w < W; ++w) {
-    int lw = nlegs - kLegsPerWave * w;
-    lw = lw < 0 ? 0 : (lw > kLegsPerWave ? kLegsPerWave : lw);
-    ncol[w] = 3 * lw;
-  }
+    for (int w = 0; w < W; ++w) {
+      int lw = nl - kLegsPerWave * w;
+      lw = lw < 0 ? 0 : (lw > kLegsPerWave ? kLegsPerWave : lw);
+      ncol[w] = 3 * lw;
+    }
+  };
   // every valid column below 60: the 60-column DPP forms (uniform)
-  const bool c60 = W == 1 && (kW1Legs <= 20 || __builtin_amdgcn_readfirstlane(ncol[0]) <= 60);
+  const bool c60 = W == 1 && (kW1Legs <= 20 || 3 * nlegs <= 60);
   const int lslot = lane / 3;
   const int comp = lane - 3 * lslot;
   const bool valid = (lane < 63) && (kLegsPerWave * wave + lslot < nlegs);
@@ -746,13 +750,10 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
   //  z lane: row 4 [0,0,1] in [fz_min, fz_max]; its slot 1 is an inert
   //  zero row with bounds [0,0] (stays z = y = 0), as are padding lanes.
   const bool xy = comp < 2;
-  float ra0 = valid ? 1.0f : 0.0f, ra1 = (valid && xy) ? 1.0f : 0.0f;
-  float rz0 = (valid && xy) ? a.mu : 0.0f, rz1 = (valid && xy) ? -a.mu : 0.0f;
-  // fz in [fz_min * c, fz_max * c] (:237, :242): c = 1 on every stance pair,
-  // 0 on the swing pairs the literal full QP keeps
-  const float cflag = valid ? (float)S.ct[4 * step + leg] : 0.0f;
-  const float rl0 = !valid ? 0.0f : (xy ? 0.0f : a.fz_min * cflag);
-  const float ru0 = !valid ? 0.0f : (xy ? INFINITY : a.fz_max * cflag);
+  // A entries (ra0, ra1, rz0, rz1) of the two slots: LDS-resident from here on
+  // (Ruiz scales them in place; registers would carry them across the setup)
+  S.arz[t] = (f4v){valid ? 1.0f : 0.0f, (valid && xy) ? 1.0f : 0.0f, (valid && xy) ? a.mu : 0.0f,
+                   (valid && xy) ? -a.mu : 0.0f};
   float rE0 = 1.0f, rE1 = 1.0f, Dr = 1.0f, cs = 1.0f;
   S.aux[0][t] = r2v;
   S.pair[t] = 4 * step + leg;
@@ -760,7 +761,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
   Row<W> K;
   float cinv = 1.0f, rho = fminf(fmaxf(p_same ? prec[NP] : a.rho, 1e-6f), 1e6f), rvi = 1.0f / rho;
   bool eq0 = false;
-  float qn[2] = {0.0f, 0.0f};
 #define RV0 (eq0 ? 1e3f * rho : rho)
 #define RVI0 (eq0 ? 1e-3f * rvi : rvi)
   // leg block sigma I + A' diag(rho) A (3x3, leg-local); scaled A entries from LDS
@@ -858,8 +858,12 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       float cnP = 0.0f;
 #pragma unroll
       for (int c = 0; c < NK; ++c) cnP = fmaxf(cnP, fabsf(KE(K, c)));
-      const float inv_n = 1.0f / (float)(n > 0 ? n : 1);
+      const int n_r = 3 * uni(S.nlegs);  // re-read: 1/n stays out of the loop-live set
+      const float inv_n = 1.0f / (float)(n_r > 0 ? n_r : 1);
       for (int it = 0; it < a.scaling; ++it) {
+        asm volatile("" ::: "memory");  // re-read the entries (not forwarded in registers)
+        const f4v arz0 = S.arz[t];
+        float ra0 = arz0.x, ra1 = arz0.y, rz0 = arz0.z, rz1 = arz0.w;
         float cnA = fmaxf(fabsf(ra0), fabsf(ra1));
         const float zmax = fmaxf(fabsf(rz0), fabsf(rz1));
         const float zm1 = lane_prev(zmax), zm2 = lane_prev(zm1);
@@ -875,6 +879,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         ra1 *= Et1 * Dt;
         rz0 *= Et0 * Dz;
         rz1 *= Et1 * Dz;
+        S.arz[t] = (f4v){ra0, ra1, rz0, rz1};
         rE0 *= Et0;
         rE1 *= Et1;
         qv *= Dt;
@@ -912,6 +917,12 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         cnP = cn2 * cs;
       }
       cinv = 1.0f / cs;
+      // fz in [fz_min * c, fz_max * c] (ConvexMpc.cpp:237, :242): c = 1 on every
+      // stance pair, 0 on the swing pairs the literal full QP keeps (computed
+      // here, not at entry: kept live across the setup they spilled)
+      const float cflag = valid ? (float)S.ct[S.pair[opaque_tid()]] : 0.0f;
+      const float rl0 = !valid ? 0.0f : (xy ? 0.0f : a.fz_min * cflag);
+      const float ru0 = !valid ? 0.0f : (xy ? INFINITY : a.fz_max * cflag);
       const float lh0 = rl0 * rE0, uh0 = ru0 * rE0;
       // slot 1: (-inf, 0] on x/y lanes (E scaling keeps 0 and inf), inert [0, 0] elsewhere
       const float lh1 = (valid && xy) ? -INFINITY : 0.0f, uh1 = 0.0f;
@@ -925,10 +936,12 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       S.aux[2][t] = rE1;
       S.zb[t] = (f4v){lh0, uh0, lh1, uh1};
       // ||D^-1 q||_inf and ||q||_inf (scaled) are constant over the iterations
-      qn[0] = fabsf(qv / Dr);
-      qn[1] = fabsf(qv);
+      float qn[2] = {fabsf(qv / Dr), fabsf(qv)};
       bmax<W, 2>(qn, S.red);
-      S.arz[t] = (f4v){ra0, ra1, rz0, rz1};
+      if (t == 0) {
+        S.qn[0] = qn[0];
+        S.qn[1] = qn[1];
+      }
       S.qs[t] = qv;
       bsync<W>();
     }
@@ -937,6 +950,8 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       float add0, add1, add2;
       leg_block(add0, add1, add2);
       const float dg = finalize_row<W, C2>(S, t, t - comp, cs * S.Dc[t], add0, add1, add2, c60, K);
+      int ncol[W];
+      col_counts(uni(S.nlegs), ncol);
       if constexpr (W == 1) {
         (void)dg;
         if (c60) {
@@ -972,7 +987,8 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         y.y = (valid && xy) ? wy[rbase + 1] / rE1 * cs : 0.0f;
         const float n1 = lane_next(x), n2 = lane_next(n1);
         const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x);
-        z = (f2v){ra0, ra1} * x + (f2v){rz0, rz1} * xz;
+        const f4v arz = S.arz[t];
+        z = (f2v){arz.x, arz.y} * x + (f2v){arz.z, arz.w} * xz;
       }
     }
     bool refactor = false;
@@ -1094,9 +1110,10 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       float o[6], r[6];
       residuals(o, r, do_rho);
       const float pri_res = o[0], dua_res = cinv * o[3];
+      const float qn0 = S.qn[0], qn1 = S.qn[1];  // set at the first factorisation, behind its barrier
       if (can_check) {
         const float eps_p = a.eps_abs + a.eps_rel * fmaxf(o[1], o[2]);
-        const float eps_d = a.eps_abs + a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
+        const float eps_d = a.eps_abs + a.eps_rel * cinv * fmaxf(fmaxf(qn0, o[4]), o[5]);
         if (pri_res < eps_p && dua_res < eps_d) {
           status = QLOCO_OK;
           break;
@@ -1104,7 +1121,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       }
       if (do_rho) {  // compute_rho_estimate + adapt_rho
         const float pn = r[0] / (fmaxf(r[1], r[2]) + 1e-30f);
-        const float dn = r[3] / (fmaxf(fmaxf(qn[1], r[4]), r[5]) + 1e-30f);
+        const float dn = r[3] / (fmaxf(fmaxf(qn1, r[4]), r[5]) + 1e-30f);
         float rho_new = rho * sqrtf(pn / (dn + 1e-30f));
         rho_new = fminf(fmaxf(rho_new, 1e-6f), 1e6f);
         if (rho_new > rho * a.rho_tol || rho_new < rho / a.rho_tol) {
@@ -1118,9 +1135,14 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         }
       }
       if (fin) {  // max_iter reached (OSQP: solved inaccurate or max_iter)
-        const float ep = 10.f * a.eps_abs + 10.f * a.eps_rel * fmaxf(o[1], o[2]);
-        const float ed = 10.f * a.eps_abs + 10.f * a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
-        status = (pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE : QLOCO_MAX_ITER;
+        // laundered: 10 eps is otherwise hoisted into two loop-live VGPRs
+        float e_abs = a.eps_abs, e_rel = a.eps_rel;
+        asm volatile("" : "+v"(e_abs), "+v"(e_rel));
+        const float ep = 10.f * e_abs + 10.f * e_rel * fmaxf(o[1], o[2]);
+        const float ed = 10.f * e_abs + 10.f * e_rel * cinv * fmaxf(fmaxf(qn0, o[4]), o[5]);
+        // block-uniform: an SGPR, not a VGPR kept live to the outputs
+        status = __builtin_amdgcn_readfirstlane((pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE
+                                                                                 : QLOCO_MAX_ITER);
         break;
       }
     }
@@ -1128,24 +1150,25 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
   }
 
   // ---------------- 10. outputs: unscale, objective, scatter to leg slots
-  const float Dr_o = S.Dc[t];
-  const int pr_o = S.pair[t];
+  const int to = opaque_tid();  // the thread index (and its byte offsets) re-derived here
+  const float Dr_o = S.Dc[to];
+  const int pr_o = S.pair[to];
   const int step_o = pr_o >> 2, leg_o = pr_o & 3;
   const float xu = valid ? x * Dr_o : 0.0f;
-  const float objp = bsum<W>(valid ? cinv * (0.5f * x * px + S.qs[t] * x) : 0.0f, S.red);
+  const float objp = bsum<W>(valid ? cinv * (0.5f * x * px + S.qs[to] * x) : 0.0f, S.red);
   const bool bad = !isfinite(objp);
   if (bad) status = QLOCO_NAN;
   if (a.u) {  // full solution (world frame), swing forces exactly 0
     float *uo = a.u + b * 12 * N;
-    for (int k = t; k < 12 * N; k += NC) uo[k] = 0.0f;
+    for (int k = to; k < 12 * N; k += NC) uo[k] = 0.0f;
     __syncthreads();
     if (valid) uo[12 * step_o + 3 * leg_o + comp] = bad ? NAN : xu;
   }
   // u0: step-0 forces; optional body frame R' u (A1RobotControl.cpp:596-599)
-  S.xs[t] = xu;
+  S.xs[to] = xu;
   bsync<W>();
-  if (t < 12) {
-    const int lg = t / 3, cp = t - 3 * lg;
+  if (to < 12) {
+    const int lg = to / 3, cp = to - 3 * lg;
     float f0 = 0.f, f1 = 0.f, f2 = 0.f;
     for (int p = 0; p < S.stepstart[1]; ++p) {
       if ((S.legtab[p] & 3) == lg) {
@@ -1156,12 +1179,15 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       }
     }
     float o = cp == 0 ? f0 : (cp == 1 ? f1 : f2);
-    if (a.output_frame == 1)  // R^T f with R = [[c,s,0],[-s,c,0],[0,0,1]]
-      o = cp == 0 ? (R00 * f0 + R10 * f1) : (cp == 1 ? (R01 * f0 + R11 * f1) : f2);
-    a.u0[b * 12 + t] = bad ? NAN : o;
+    if (a.output_frame == 1) {  // R^T f with R = [[c,s,0],[-s,c,0],[0,0,1]]
+      // the rotation re-derived from the yaw in LDS (not kept live since section 3)
+      const float oy = S.x0[2], oc = cosf(oy), os = sinf(oy);
+      o = cp == 0 ? (oc * f0 - os * f1) : (cp == 1 ? (os * f0 + oc * f1) : f2);
+    }
+    a.u0[b * 12 + to] = bad ? NAN : o;
   }
   if (prec) {  // the persistent record for the next call
-    for (int k = t; k < NP + 4; k += NC) prec[k] = 0.0f;
+    for (int k = to; k < NP + 4; k += NC) prec[k] = 0.0f;
     __syncthreads();
     if (valid) {
       const int vidx = 12 * step_o + 3 * leg_o + comp, rbase = 20 * step_o + 5 * leg_o + 2 * comp;
@@ -1170,15 +1196,15 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       prec[84 * N + vidx] = q_raw;
       prec[12 * N + rbase] = z.x;
       prec[32 * N + rbase] = y.x;
-      prec[64 * N + rbase] = cinv * S.aux[1][t] * y.x;
+      prec[64 * N + rbase] = cinv * S.aux[1][to] * y.x;
       if (xy) {
         prec[12 * N + rbase + 1] = z.y;
         prec[32 * N + rbase + 1] = y.y;
-        prec[64 * N + rbase + 1] = cinv * S.aux[2][t] * y.y;
+        prec[64 * N + rbase + 1] = cinv * S.aux[2][to] * y.y;
       }
     }
-    for (int k = t; k < 4 * N; k += NC) prec[96 * N + k] = S.ct[k] ? 1.0f : 0.0f;
-    if (t == 0) {
+    for (int k = to; k < 4 * N; k += NC) prec[96 * N + k] = S.ct[k] ? 1.0f : 0.0f;
+    if (to == 0) {
       prec[NP] = rho;
       prec[NP + 1] = 1.0f;
     }
@@ -1187,16 +1213,16 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
     const int nu = 12 * N, ncn = 20 * N;
     float *wx = a.warm + b * (nu + ncn);
     float *wy = wx + nu;
-    for (int k = t; k < nu + ncn; k += NC) wx[k] = 0.0f;
+    for (int k = to; k < nu + ncn; k += NC) wx[k] = 0.0f;
     __syncthreads();
     if (valid) {
       wx[12 * step_o + 3 * leg_o + comp] = xu;
       const int rbase = 20 * step_o + 5 * leg_o + 2 * comp;
-      wy[rbase] = cinv * S.aux[1][t] * y.x;
-      if (xy) wy[rbase + 1] = cinv * S.aux[2][t] * y.y;
+      wy[rbase] = cinv * S.aux[1][to] * y.x;
+      if (xy) wy[rbase + 1] = cinv * S.aux[2][to] * y.y;
     }
   }
-  if (t == 0) {
+  if (to == 0) {
     if (a.status) a.status[b] = status;
     if (a.iters) a.iters[b] = iter;
     if (a.rho_updates) a.rho_updates[b] = rho_updates;

@@ -149,8 +149,7 @@ __device__ __forceinline__ void lit_invert(LitLds &S, int lane, int ncol, Row<1>
     constexpr int k = decltype(kc)::value;
     asm volatile("" : "+s"(nc));
     if (k >= nc) return;
-    int tt = lane;
-    asm volatile("" : "+v"(tt));
+    const int tt = fresh_lane();
     lsync();
     const f4v r0 = S.bc[lane & 15];
     const float v = K.k[k];
@@ -209,13 +208,15 @@ __device__ __forceinline__ void chol6(const float (&a)[6][6], float (&L)[6][6], 
 // VALU) instead of hoisted to the kernel entry and kept live -- at 128 VGPRs
 // the hoisted offsets were the setup's scratch spills.
 #define QL_LIT_LANE_INDICES(LX)                                                                    \
-  int LX = threadIdx.x;                                                                            \
-  asm volatile("" : "+v"(LX));                                                                     \
+  const int LX = fresh_lane();                                                                     \
   const int jr = LX < 60 ? LX / 6 : kLitN - 1, sr = LX < 60 ? LX - 6 * (LX / 6) : 0;               \
   const bool wvalid = LX < nw;                                                                     \
   const int step[2] = {LX < 60 && LX < nvar ? LX / 12 : 0, LX < 60 && 60 + LX < nvar ? (60 + LX) / 12 : 0}; \
   const int leg[2] = {LX < 60 && LX < nvar ? (LX % 12) / 3 : 0, LX < 60 && 60 + LX < nvar ? ((60 + LX) % 12) / 3 : 0}; \
-  (void)jr; (void)sr; (void)wvalid; (void)step; (void)leg
+  const int comp = LX % 3;                                                                         \
+  const bool xy = comp < 2;                                                                        \
+  const bool valid[2] = {LX < 60 && LX < nvar, LX < 60 && 60 + LX < nvar};                         \
+  (void)jr; (void)sr; (void)wvalid; (void)step; (void)leg; (void)comp; (void)xy; (void)valid
 
 // WS: a warm-start mode (1 or 2) may be set (the persistent record of
 // DESIGN.md §3c, literal semantics: the update path on every call).
@@ -554,7 +555,10 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       lsync();
     }
   }
-  const float cinv = 1.0f / cs;
+  // block-uniform scalars live in SGPRs (a VGPR copy would be kept, and
+  // spilled, across the whole ADMM loop)
+  cs = sgpr_f(cs);
+  const float cinv = sgpr_f(1.0f / cs);
   bool eq0[2];
   float qn[2] = {0.0f, 0.0f};
 #pragma unroll
@@ -573,7 +577,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   // row scaling E of a slot's two rows, from A~ = E A D (each row's entry in
   // its own variable's column is 1 before scaling)
   auto row_e = [&](int h) -> f2v {
-    const f4v arz = S.arz[h][lane];
+    const f4v arz = S.arz[h][fresh_lane()];
     const float d = Dr[h];
     return (f2v){valid[h] ? arz.x / d : 1.0f, (valid[h] && xy) ? arz.y / d : 1.0f};
   };
@@ -587,7 +591,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   // the factorisation's bound); padding wrench lanes get zeros
   // through their K0 / K2 weights and masks
   // this lane's variables' wrench columns (omega rows = lo.xyz, v row = dtm at comp)
-  float rho = fminf(fmaxf(p_same ? prec[NP] : a.rho, 1e-6f), 1e6f);
+  float rho = sgpr_f(fminf(fmaxf(p_same ? prec[NP] : a.rho, 1e-6f), 1e6f));
 
   // ---------------- 6. ADMM (osqp_solve) with its (re)factorisations
   float x[2] = {0.0f, 0.0f};
@@ -607,8 +611,10 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   // P~ x (scaled) per slot: c D (Vu' G Vu + R) D x through the wrench rows
   auto p_times_x = [&](float (&out)[2]) {
     QL_LIT_LANE_INDICES(lxp);
+    float drp[2] = {Dr[0], Dr[1]};  // opaque: cs D is not hoisted into the loop-live set
+    asm volatile("" : "+v"(drp[0]), "+v"(drp[1]));
 #pragma unroll
-    for (int h = 0; h < 2; ++h) S.av[h][lane] = valid[h] ? x[h] * Dr[h] : 0.0f;
+    for (int h = 0; h < 2; ++h) S.av[h][lxp] = valid[h] ? x[h] * drp[h] : 0.0f;
     lsync();
     // w = Vu (D x): wrench row (jr, sr) sums its step's 12 variables
     float wr = 0.0f;
@@ -624,14 +630,14 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       for (int w = 0; w < 12; ++w) wr = fmaf(bv[w], uv[w], wr);
       wr = wvalid ? wr : 0.0f;
     }
-    S.wv[lane] = wr;
+    S.wv[lxp] = wr;
     lsync();
     // Te w per row (needs the step's 6 wrench values)
     {
       float tw = 0.0f;
 #pragma unroll
       for (int t = 0; t < 6; ++t) tw = fmaf(S.Te[sr][t], S.wv[6 * jr + t], tw);
-      reinterpret_cast<float *>(&S.bc[0])[lane] = wvalid ? tw : 0.0f;  // Te w (bc is free in a check)
+      reinterpret_cast<float *>(&S.bc[0])[lxp] = wvalid ? tw : 0.0f;  // Te w (bc is free in a check)
     }
     lsync();
     // (G w)[(jr, sr)] = Qb_s sum_k K0(jr,k) w(k,sr) + sum_k K2(jr,k) (Te w_k)_sr
@@ -648,7 +654,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       gw = wvalid ? fmaf(qb, s0, s2) : 0.0f;
     }
     lsync();
-    S.wv[lane] = gw;
+    S.wv[lxp] = gw;
     lsync();
     // Vu' (G w) + R (D x), then c D (...)
 #pragma unroll
@@ -656,24 +662,25 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       float acc = 0.0f;
       if (valid[h]) {
         const float *gs = &S.wv[6 * step[h]];
-        const int wc = lane % 12;  // the variable's column of Bb (both slots: 60 = 5 x 12)
+        const int wc = lxp % 12;  // the variable's column of Bb (both slots: 60 = 5 x 12)
         acc = S.Bb[0][wc] * gs[0] + S.Bb[1][wc] * gs[1] + S.Bb[2][wc] * gs[2] + dtm * gs[3 + comp];
-        acc = fmaf(S.r2[3 * leg[h] + comp], x[h] * Dr[h], acc);  // valid slot: r2 of its leg
+        acc = fmaf(S.r2[3 * leg[h] + comp], x[h] * drp[h], acc);  // valid slot: r2 of its leg
       }
-      out[h] = cs * Dr[h] * acc;
+      out[h] = cs * drp[h] * acc;
     }
     lsync();
   };
 
   auto residuals = [&](float (&o)[6], float (&r)[6], bool want_r) {
     p_times_x(px);
+    QL_LIT_LANE_INDICES(lxr);
 #pragma unroll
     for (int k = 0; k < 6; ++k) o[k] = r[k] = 0.0f;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const float Drl = Dr[h];
       const float Dinvl = __builtin_amdgcn_rcpf(Drl);
-      const f4v arz = S.arz[h][lane];
+      const f4v arz = S.arz[h][lxr];
       // E^-1 of the slot's rows from A~ = E A D (unit own-column entries)
       const f2v Einv = {valid[h] ? Drl * __builtin_amdgcn_rcpf(arz.x) : 1.0f,
                         (valid[h] && xy) ? Drl * __builtin_amdgcn_rcpf(arz.y) : 1.0f};
@@ -741,15 +748,19 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     {
       // opaque per factorisation: nothing derived from these is hoisted out of
       // the refactor loop (it would stay live through the ADMM iterations)
-      int ln = lane;
-      float csf = cs, dinv[2] = {Dinv[0], Dinv[1]};
-      asm volatile("" : "+v"(ln), "+v"(csf), "+v"(dinv[0]), "+v"(dinv[1]));
+      int ln = fresh_lane();
+      float csf = cs;
+      asm volatile("" : "+v"(ln), "+v"(csf));
       QL_LIT_LANE_INDICES(lxf);
       // this lane's row of W0^-1 for slot h (W0 = D^-1 (sigma I + A~' rho A~) D^-1 +
       // c R, 3 x 3 per leg): written for the U rows, recomputed for the
       // iteration coefficients after the T phase (its LDS is the T passes')
+      // (D^-1 and c re-laundered per call: the first call's copies do not stay
+      // live across S^-1 for the second)
       auto w0_inv_row = [&](int h, float &i0, float &i1, float &i2) {
-        const f4v arz = S.arz[h][lane];
+        float dinv_h = Dinv[h], csw = cs;
+        asm volatile("" : "+v"(dinv_h), "+v"(csw));
+        const f4v arz = S.arz[h][lxf];
         const float rv0 = eq0[h] ? 1e3f * rho : rho, rv1 = rho;
         const float d_own = rv0 * arz.x * arz.x + rv1 * arz.y * arz.y;
         const float d_oz = rv0 * arz.x * arz.z + rv1 * arz.y * arz.w;
@@ -764,10 +775,10 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         } else {
           m0 = oz2; m1 = oz1; m2 = d_own + zz1 + zz2 + sigma;
         }
-        const Triple dd = triple(dinv[h], comp);
+        const Triple dd = triple(dinv_h, comp);
         // W0 row = D^-1 M D^-1 + c R (diagonal)
-        float w0 = dinv[h] * m0 * dd.v0, w1 = dinv[h] * m1 * dd.v1, w2 = dinv[h] * m2 * dd.v2;
-        const float cr = csf * (valid[h] ? S.r2[3 * leg[h] + comp] : 0.0f);
+        float w0 = dinv_h * m0 * dd.v0, w1 = dinv_h * m1 * dd.v1, w2 = dinv_h * m2 * dd.v2;
+        const float cr = csw * (valid[h] ? S.r2[3 * leg[h] + comp] : 0.0f);
         w0 += comp == 0 ? cr : 0.0f;
         w1 += comp == 1 ? cr : 0.0f;
         w2 += comp == 2 ? cr : 0.0f;
@@ -790,9 +801,9 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       for (int h = 0; h < 2; ++h) {
         float i0, i1, i2;
         w0_inv_row(h, i0, i1, i2);
-        S.w0i[0][h][lane] = i0;
-        S.w0i[1][h][lane] = i1;
-        S.w0i[2][h][lane] = i2;
+        S.w0i[0][h][lxf] = i0;
+        S.w0i[1][h][lxf] = i1;
+        S.w0i[2][h][lxf] = i2;
       }
       lsync();
       // U_j rows: wrench lane (jr, sr): U[sr][t] = sum_w Bb[sr][w] (W0^-1 Bb')[w][t]
@@ -838,7 +849,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
             lisr = (c == sr) ? Li[r][c] : lisr;
           }
           Lcol[r] = lsr;
-          if (lane < 60) {
+          if (lxf < 60) {
             if (r >= sr) {
               S.Lt[jr][tri(sr) - sr + r] = lsr;   // column sr of L_j
               S.Li[jr][tri(sr) - sr + r] = lisr;  // column sr of L_j^-1
@@ -877,7 +888,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
           const float dg = wvalid ? 1.0f + csf * fmaf(kk.x, da, kk.y * db) : 1.0f;
           sS = 1.0f / wmax_nonneg(dg);
         }
-        cS = csf * sS;
+        cS = sgpr_f(csf * sS);
 #pragma unroll
         for (int c = 0; c < 60; ++c) {
           const int k = c / 6, t = c - 6 * (c / 6);
@@ -897,7 +908,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         for (int c = 60; c < 64; ++c) T.k[c] = 0.0f;
       }
       // S^-1 in place
-      lit_invert(S, lane, nw, T);
+      lit_invert(S, lxf, nw, T);
       // Z = S^-1 blockdiag(L_k^-1), this lane's row in place (L_k^-1 lower
       // triangular: column (k, t) from the columns (k, t' >= t))
 #pragma unroll
@@ -918,11 +929,9 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       // M = L Z and Te M (= (Te L) Z), the horizon sums with K0 / K2 give
       // (cG M)[(j,s)] = c (Qb_s sum_k K0(j,k) M[(k,s)] + sum_k K2(j,k) (Te M)[(k,s)])
       {
-        float lrow[6], tlrow[6];  // row sr of L_jr and of Te L_jr (Te L from the packed columns)
+        float tlrow[6];  // row sr of Te L_jr (from the packed columns); L's row is re-read per pass
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
-          const float lv = S.Lt[jr][tri(c) - c + (sr > c ? sr : c)];  // in bounds for every lane
-          lrow[c] = c <= sr ? lv : 0.0f;
           float tl = 0.0f;
 #pragma unroll
           for (int r = c; r < 6; ++r) tl = fmaf(S.Te[sr][r], S.Lt[jr][tri(c) - c + r], tl);
@@ -931,19 +940,20 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         const float qb = S.q2[6 + sr];
 #pragma unroll
         for (int g = 0; g < 15; ++g) {
-          S.zc[lane] = (f4v){T.k[4 * g], T.k[4 * g + 1], T.k[4 * g + 2], T.k[4 * g + 3]};
+          S.zc[lxf] = (f4v){T.k[4 * g], T.k[4 * g + 1], T.k[4 * g + 2], T.k[4 * g + 3]};
           lsync();
           f4v m = (f4v)(0.0f), tm = (f4v)(0.0f);
 #pragma unroll
           for (int s2 = 0; s2 < 6; ++s2) {
             const f4v zr = S.zc[6 * jr + s2];
-            m = __builtin_elementwise_fma((f4v)(lrow[s2]), zr, m);
+            const float lv = S.Lt[jr][tri(s2) - s2 + (sr > s2 ? sr : s2)];  // in bounds for every lane
+            m = __builtin_elementwise_fma((f4v)(s2 <= sr ? lv : 0.0f), zr, m);
             tm = __builtin_elementwise_fma((f4v)(tlrow[s2]), zr, tm);
           }
           // L Z overwrites Z: the wave's LDS reads above complete in order first
           asm volatile("" ::: "memory");
-          S.zc[lane] = m;
-          S.tc[lane] = tm;
+          S.zc[lxf] = m;
+          S.tc[lxf] = tm;
           lsync();
           f4v o0 = (f4v)(0.0f), o2 = (f4v)(0.0f);
 #pragma unroll
@@ -975,8 +985,12 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     for (;;) {
       if (iter < a.max_iter) {
         int next = a.max_iter;
-        if (ctm) next = min(next, (iter / ctm + 1) * ctm);
-        if (interval) next = min(next, (iter / interval + 1) * interval);
+        // opaque divisors: the reciprocal constants of the two divisions are
+        // recomputed per block instead of held in VGPRs for the whole kernel
+        int ctl = ctm, itl = interval;
+        asm volatile("" : "+s"(ctl), "+s"(itl));
+        if (ctl) next = min(next, (iter / ctl + 1) * ctl);
+        if (itl) next = min(next, (iter / itl + 1) * itl);
         const float rho_s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rho)));
         const float rvb_s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, 1.0f / rho)));
         const float zlo = a.fz_max > 0.0f ? a.fz_min / a.fz_max : 0.0f;  // z rows: lower = zlo upper
@@ -996,7 +1010,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
           float av[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const f4v arz = S.arz[h][lane];
+            const f4v arz = S.arz[h][lxi];
             const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
             const f2v rv = {rva[h][0], rva[h][1]};
             const f2v w = __builtin_elementwise_fma(rv, z[h], -y[h]);
@@ -1014,7 +1028,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
                   : "v"(tz), "v"(m2));
             }
             av[h] = tdot(Dinv[h] * rhs, W1[h]);  // W0^-1 D^-1 rhs
-            S.av[h][lane] = av[h];
+            S.av[h][lxi] = av[h];
           }
           lsync();
           // v = Vu a: wrench row (jr, sr) over its step's 12 variables
@@ -1035,22 +1049,22 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
             }
             wr = w0 + w1;
           }
-          reinterpret_cast<float *>(&S.bc[0])[lane] = wr;
+          reinterpret_cast<float *>(&S.bc[0])[lxi] = wr;
           lsync();
           // s = T v (DPP broadcast matvec, 60 columns)
           float sv;
           {
-            const f4v r0 = S.bc[lane & 15];
+            const f4v r0 = S.bc[lxi & 15];
             float acc0, acc1;
             QL_DPP_MATVEC60_2(acc0, acc1, r0, T.k, 0);
             sv = acc0 + acc1;
           }
-          S.wv[lane] = sv;
+          S.wv[lxi] = sv;
           lsync();
           // x~ = D^-1 a - D^-1 W0^-1 Vu' s, then update_x / update_z / update_y; the
           // variable's omega rows of B_d from LDS (a padding slot's are harmless:
           // its leg's B1 coefficients are zero)
-          const float bw0 = S.Bb[0][lane % 12], bw1 = S.Bb[1][lane % 12], bw2 = S.Bb[2][lane % 12];
+          const float bw0 = S.Bb[0][lxi % 12], bw1 = S.Bb[1][lxi % 12], bw2 = S.Bb[2][lxi % 12];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const float *gs = &S.wv[6 * step[h]];
@@ -1060,9 +1074,9 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
             const float sf = comp == 0 ? s23.y : (comp == 1 ? s45.x : s45.y);
             const float tv = fmaf(bw0, s01.x, fmaf(bw1, s01.y, fmaf(bw2, s23.x, dtm * sf)));
             const float xt = Dinv[h] * (av[h] - tdot(tv, W1[h]));  // D^-1 (a - W0^-1 t)
-            const f4v arz = S.arz[h][lane];
+            const f4v arz = S.arz[h][lxi];
             const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
-            const float hi = S.zh[h][lane];
+            const float hi = S.zh[h][lxi];
             const f2v bnd = {xy ? 0.0f : zlo * hi, hi};
             const float n1 = lane_next(xt), n2 = lane_next(n1);
             const float xtz = comp == 0 ? n2 : n1;
@@ -1099,7 +1113,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         float rho_new = rho * sqrtf(pn / (dn + 1e-30f));
         rho_new = fminf(fmaxf(rho_new, 1e-6f), 1e6f);
         if (rho_new > rho * a.rho_tol || rho_new < rho / a.rho_tol) {
-          rho = rho_new;
+          rho = sgpr_f(rho_new);
           rho_updates++;
           if (!fin) {
             refactor = true;
@@ -1108,9 +1122,12 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         }
       }
       if (fin) {
-        const float ep = 10.f * a.eps_abs + 10.f * a.eps_rel * fmaxf(o[1], o[2]);
-        const float ed = 10.f * a.eps_abs + 10.f * a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
-        status = (pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE : QLOCO_MAX_ITER;
+        float e_abs = a.eps_abs, e_rel = a.eps_rel;  // laundered: 10 eps is not hoisted into VGPRs
+        asm volatile("" : "+v"(e_abs), "+v"(e_rel));
+        const float ep = 10.f * e_abs + 10.f * e_rel * fmaxf(o[1], o[2]);
+        const float ed = 10.f * e_abs + 10.f * e_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
+        status = __builtin_amdgcn_readfirstlane((pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE
+                                                                                 : QLOCO_MAX_ITER);
         break;
       }
     }
@@ -1118,6 +1135,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   }
 
   // ---------------- 7. outputs: unscale, objective, leg slots (A1RobotControl.cpp:593-599)
+  const int lane_o = fresh_lane();
   float xu[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) xu[h] = valid[h] ? x[h] * Dr[h] : 0.0f;
@@ -1131,7 +1149,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     float *uo = a.u + b * 12 * N;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
-      if (valid[h]) uo[60 * h + lane] = bad ? NAN : xu[h];
+      if (valid[h]) uo[60 * h + lane_o] = bad ? NAN : xu[h];
   }
   // u0: step-0 forces (variables 0..11 = slot 0, lanes 0..11); optional body frame R' u
   {
@@ -1140,17 +1158,17 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     const float f0 = comp == 0 ? xu[0] : (comp == 1 ? p1 : p2);
     const float f1 = comp == 0 ? n1 : (comp == 1 ? xu[0] : p1);
     const float f2 = comp == 0 ? n2 : (comp == 1 ? n1 : xu[0]);
-    if (lane < 12) {
+    if (lane_o < 12) {
       float o = xu[0];
       if (a.output_frame == 1) {  // R^T f with R = [[c,s,0],[-s,c,0],[0,0,1]], recomputed here
         const float yw = S.x0[2], cw = cosf(yw), sw = sinf(yw);
         o = comp == 0 ? (cw * f0 - sw * f1) : (comp == 1 ? (sw * f0 + cw * f1) : f2);
       }
-      a.u0[b * 12 + lane] = bad ? NAN : o;
+      a.u0[b * 12 + lane_o] = bad ? NAN : o;
     }
   }
   if (prec) {  // the persistent record for the next call (layout QLOCO_SRBD_PERSIST_LEN)
-    for (int k = lane; k < NP + 4; k += 64) prec[k] = 0.0f;
+    for (int k = lane_o; k < NP + 4; k += 64) prec[k] = 0.0f;
     __syncthreads();
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1169,8 +1187,8 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         prec[64 * N + rbase + 1] = cinv * e.y * y[h].y;
       }
     }
-    for (int k = lane; k < 4 * N; k += 64) prec[96 * N + k] = S.ctf[k];
-    if (lane == 0) {
+    for (int k = lane_o; k < 4 * N; k += 64) prec[96 * N + k] = S.ctf[k];
+    if (lane_o == 0) {
       prec[NP] = rho;
       prec[NP + 1] = 1.0f;
     }
@@ -1179,7 +1197,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     const int nu = 12 * N, ncn = 20 * N;
     float *wx = a.warm + b * (nu + ncn);
     float *wy = wx + nu;
-    for (int k = lane; k < nu + ncn; k += 64) wx[k] = 0.0f;
+    for (int k = lane_o; k < nu + ncn; k += 64) wx[k] = 0.0f;
     __syncthreads();
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1191,7 +1209,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       if (xy) wy[rbase + 1] = cinv * e.y * y[h].y;
     }
   }
-  if (lane == 0) {
+  if (lane_o == 0) {
     if (a.status) a.status[b] = status;
     if (a.iters) a.iters[b] = iter;
     if (a.rho_updates) a.rho_updates[b] = rho_updates;
