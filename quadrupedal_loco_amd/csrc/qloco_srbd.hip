@@ -496,7 +496,6 @@ __device__ __forceinline__ void fill_k0k2(SrbdLds<W, NM> &S, int N, float Nf, in
 // pivot, the pivot value through LDS.
 template <int H, int C2, int NM>
 __device__ __forceinline__ void invert_w2_half(SrbdLds<2, NM> &S, int t, int nw, Row<2> &K) {
-  const int lane = t & 63;
   int nc = __builtin_amdgcn_readfirstlane(nw);
 #pragma unroll
   for (int kk = 0; kk < (H == 1 ? 4 * C2 : 64); ++kk) {
@@ -512,7 +511,9 @@ __device__ __forceinline__ void invert_w2_half(SrbdLds<2, NM> &S, int t, int nw,
     S.colv[buf][tt] = v;  // the pivot A_kk for the other wave (no divergent store)
     __syncthreads();
     const float p = S.colv[buf][k];
-    const f4v r0 = S.bc[buf][lane & 15], r1 = S.bc[buf][16 + (lane & 15)];
+    // chunk index from the per-pivot opaque copy: its LDS offset is not
+    // hoisted to kernel entry (it was reloaded from scratch every pivot)
+    const f4v r0 = S.bc[buf][tt & 15], r1 = S.bc[buf][16 + (tt & 15)];
     const float pinv = __builtin_amdgcn_rcpf(p);
     const float ng = -((tt == k) ? (1.0f - pinv) : v * pinv);
     QL_DPP_GJ64(K.k, 0, r0, ng);
