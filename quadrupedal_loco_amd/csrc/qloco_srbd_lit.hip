@@ -720,6 +720,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
 
   // warm start (x, z, y) before the first factorisation
   if (WS) {
+    QL_LIT_LANE_INDICES(lxs);  // record addresses derived here, not shared with the write-back
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int vidx = 12 * step[h] + 3 * leg[h] + comp, rbase = 20 * step[h] + 5 * leg[h] + 2 * comp;
@@ -738,7 +739,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         y[h].y = (valid[h] && xy) ? wy[rbase + 1] / e.y * cs : 0.0f;
         const float n1 = lane_next(x[h]), n2 = lane_next(n1);
         const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x[h]);
-        const f4v arz = S.arz[h][lane];
+        const f4v arz = S.arz[h][lxs];
         z[h] = (f2v){arz.x, arz.y} * x[h] + (f2v){arz.z, arz.w} * xz;
       }
     }
@@ -1168,6 +1169,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     }
   }
   if (prec) {  // the persistent record for the next call (layout QLOCO_SRBD_PERSIST_LEN)
+    QL_LIT_LANE_INDICES(lxo);  // fresh indices: no address kept live from the warm start
     for (int k = lane_o; k < NP + 4; k += 64) prec[k] = 0.0f;
     __syncthreads();
 #pragma unroll
@@ -1194,6 +1196,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     }
   }
   if (WS && a.warm_start == 1) {
+    QL_LIT_LANE_INDICES(lxo);
     const int nu = 12 * N, ncn = 20 * N;
     float *wx = a.warm + b * (nu + ncn);
     float *wy = wx + nu;

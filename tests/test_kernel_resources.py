@@ -25,7 +25,7 @@ SPILL_BOUND = {
     "_ZN5qloco16srbd_admm_kernelILi2ELi3ELb0ELi20ELi15EEEvNS_8SrbdArgsE": 33,   # C2 = 15 bucket
     "_ZN5qloco20srbd_admm_big_kernelILb1ELi128EEEvNS_8SrbdArgsE": 43,           # warm wide kernel
     "_ZN5qloco20srbd_admm_big_kernelILb0ELi120EEEvNS_8SrbdArgsE": 3,
-    "_ZN5qloco15srbd_lit_kernelILb1EEEvNS_8SrbdArgsE": 45,                      # literal, persistent
+    "_ZN5qloco15srbd_lit_kernelILb1EEEvNS_8SrbdArgsE": 28,                      # literal, persistent
     "_ZN5qloco15srbd_lit_kernelILb0EEEvNS_8SrbdArgsE": 24,                      # literal headline
 }
 # four waves per SIMD: 128 VGPRs and 16 one-wave workgroups' LDS per CU
