@@ -967,7 +967,10 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
     }
     if (first) {
       first = false;
-      const int vidx = 12 * step + 3 * leg + comp, rbase = 20 * step + 5 * leg + 2 * comp;
+      // record offsets from an opaque thread copy: no per-lane record address
+      // is kept live from the entry's reads of the record
+      const int tf = opaque_tid(), pf = S.pair[tf], lf = tf & 63, cf = lf - 3 * (lf / 3);
+      const int vidx = 12 * (pf >> 2) + 3 * (pf & 3) + cf, rbase = 20 * (pf >> 2) + 5 * (pf & 3) + 2 * cf;
       if (p_same) {
         // live workspace (osqp_solve without cold start): the scaled
         // iterates of the last call as they are
