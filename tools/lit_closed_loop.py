@@ -33,15 +33,20 @@ for t, (x0, xr, ft, ct) in enumerate(seq):
     rec = gpu.record.cpu().numpy()
     for b in range(B):
         ub, info = orc[b].step(x0[b], xr[b], ft[b], ct[b])
-        _, dF, dM, dX = _traj_metrics(u[b], ub, x0[b], xr[b], ft[b], ct[b], N)
+        du0, dF, dM, dX = _traj_metrics(u[b], ub, x0[b], xr[b], ft[b], ct[b], N)
         r64 = orc[b].rec[100 * N]
-        rows.append((t, b, int(its[b]), info.iters, dF, dM, dX, rec[b, 100 * N] / r64))
+        rows.append((t, b, int(its[b]), info.iters, dF, dM, dX, rec[b, 100 * N] / r64, du0))
 a = np.array(rows)
 same = a[:, 2] == a[:, 3]
 print("lib %s  N=%d B=%d T=%d: same iters %.3f  rho within 10%% %.3f" % (
     os.environ.get("QLOCO_LIB", "product"), N, B, T, same.mean(), (np.abs(a[:, 7] - 1) <= 0.1).mean()))
-for k, nm in ((4, "dF"), (5, "dM"), (6, "dX")):
+for k, nm in ((4, "dF"), (5, "dM"), (6, "dX"), (8, "du0")):
     print("  %s p50 %.3g p90 %.3g p99 %.3g max %.3g" % (nm, *np.percentile(a[:, k], [50, 90, 99]), a[:, k].max()))
+for nm, sel in (("same-check", same), ("check-apart", ~same)):
+    v = a[sel, 8]
+    if v.size:
+        print("  du0 %-11s n %4d p95 %.3g max %.3g  <=0.5N %.4f" % (nm, v.size, np.percentile(v, 95), v.max(),
+                                                                   np.mean(v <= 0.5)))
 worst = a[np.argsort(-a[:, 4])[:8]]
 for r in worst:
-    print("  t=%2d b=%2d it %4d/%4d dF %6.2f dM %5.2f dX %.4f rho ratio %.3f" % tuple(r))
+    print("  t=%2d b=%2d it %4d/%4d dF %6.2f dM %5.2f dX %.4f rho ratio %.3f du0 %.3f" % tuple(r))

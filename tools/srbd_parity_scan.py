@@ -79,6 +79,14 @@ def main(cases, literal=False):
             v = R[:, k]
             print("  %-9s p50 %10.4g p90 %10.4g max %10.4g min %10.4g" % (
                 nm, np.percentile(v, 50), np.percentile(v, 90), v.max(), v.min()))
+        # u0 (the forces compute_grf returns, A1RobotControl.cpp:593-599) split by
+        # whether both runs stopped at the same termination check
+        for nm, sel in (("same-check", R[:, 15] == 0), ("check-apart", R[:, 15] != 0)):
+            v = R[sel, 0]
+            if v.size:
+                print("  du0 %-11s n %5d  p50 %9.4g p95 %9.4g p99 %9.4g max %9.4g  <=0.5N %.4f  <=2N %.4f" % (
+                    nm, v.size, *np.percentile(v, [50, 95, 99]), v.max(), np.mean(v <= 0.5),
+                    np.mean(v <= 2.0)))
         sys.stdout.flush()
 
 
