@@ -448,6 +448,15 @@ int qloco_mgpu_shard(int64_t total, int32_t world, int32_t rank, int32_t mode, i
  * world) the padded shard: rows[g] = owner * P + position.  Host only (the
  * device reorder uses the same map). */
 int qloco_mgpu_gather_rows(int64_t total, int32_t world, int32_t mode, int64_t *rows);
+/* The device half of qloco_mgpu_solve's step 3, for a caller that runs its
+ * own all-gather (e.g. torch.distributed): `stage` holds the gathered
+ * (world x P x width) shard rows, P = ceil(total / world), width 12 (u0) or
+ * 14 (u0, then status and iterations as raw int32 bits); writes u0_all
+ * [total*12] and, for width 14, status_all / iters_all [total] (optional) in
+ * global id order -- the map of qloco_mgpu_gather_rows.  Device pointers,
+ * stream-ordered on `stream`. */
+int qloco_mgpu_reorder(int64_t total, int32_t world, int32_t mode, int32_t width, const float *stage,
+                       float *u0_all, int32_t *status_all, int32_t *iters_all, void *stream);
 /* Rank 0: a new communicator id; the caller ships the bytes to every rank. */
 int qloco_mgpu_unique_id(uint8_t *id /* [QLOCO_MGPU_ID_BYTES] */);
 /* Collective: every rank, with its device current, the same id / world /

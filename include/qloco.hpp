@@ -70,7 +70,10 @@ class DeviceArena {
 // ------------------------------------------------------------------------
 // QPsolver / QPsolver_EiQuadProg (QPBaseClass.cpp:20-56): min 0.5 x'Gx + g0'x
 // s.t. CE'x + ce0 = 0, CI'x + ci0 >= 0 (EiQuadProg.hpp:15-36), quirk-compatible
-// Goldfarb-Idnani in fp64 on the GPU.  n <= 16, p <= 16, m <= 64.
+// Goldfarb-Idnani in fp64 on the GPU.  Capacity n <= 64, p <= 64, m <= 320
+// (qloco_gi_limits; the reference's QPBaseClass asserts nVars <= 60, nIneq <=
+// 300, QPBaseClass.cpp:111-112): gi_kernel up to n, p <= 16 / m <= 64,
+// gi_wide_kernel above that.
 class QPsolverGpu {
  public:
   explicit QPsolverGpu(int max_batch = 1);

@@ -97,6 +97,7 @@ SIGNATURES = {
     "qloco_a1_qp_solve": (C.c_int, [C.POINTER(A1Params), i64] + [vp] * 9),
     "qloco_mgpu_shard": (C.c_int, [i64, i32, i32, i32, vp, vp, vp]),
     "qloco_mgpu_gather_rows": (C.c_int, [i64, i32, i32, vp]),
+    "qloco_mgpu_reorder": (C.c_int, [i64, i32, i32, i32, vp, vp, vp, vp, vp]),
     "qloco_mgpu_unique_id": (C.c_int, [vp]),
     "qloco_mgpu_init": (C.c_int, [vp, vp, i32, i32, i64, i32]),
     "qloco_mgpu_info": (C.c_int, [vp, vp, vp, vp, vp]),

@@ -302,11 +302,21 @@ extern "C" int qloco_mgpu_solve(qloco_mgpu *h, const qloco_srbd_spec *spec, cons
   const ncclResult_t e = r->all_gather(sendbuf, recv, (size_t)(h->P * width), ncclFloat32, h->comm, st);
   if (e != ncclSuccess) return rccl_fail(r, "ncclAllGather", e);
   // 3. global id order
-  if (!direct) {
-    const int64_t n = h->total * 12;
-    hipLaunchKernelGGL(mgpu_unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                       h->total, h->world, h->mode, h->P, width, h->stage, u0_all, status_all, iters_all);
-    QLOCO_HIP_CHECK(hipGetLastError(), "mgpu_unpack_kernel launch");
-  }
+  if (!direct) return qloco_mgpu_reorder(h->total, h->world, h->mode, width, h->stage, u0_all,
+                                         status_all, iters_all, stream);
+  return QLOCO_OK;
+}
+
+extern "C" int qloco_mgpu_reorder(int64_t total, int32_t world, int32_t mode, int32_t width,
+                                  const float *stage, float *u0_all, int32_t *status_all,
+                                  int32_t *iters_all, void *stream) {
+  if (total < 1 || world < 1 || (mode != QLOCO_SHARD_CONTIGUOUS && mode != QLOCO_SHARD_INTERLEAVED))
+    return QLOCO_ERR_ARG;
+  if ((width != 12 && width != 14) || !stage || !u0_all) return QLOCO_ERR_ARG;
+  const int64_t n = total * 12;
+  hipLaunchKernelGGL(mgpu_unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, total, (int)world, (int)mode, mgpu_padded(total, world),
+                     (int)width, stage, u0_all, status_all, iters_all);
+  QLOCO_HIP_CHECK(hipGetLastError(), "mgpu_unpack_kernel launch");
   return QLOCO_OK;
 }

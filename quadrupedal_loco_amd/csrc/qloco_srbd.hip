@@ -1369,10 +1369,19 @@ struct SrbdScratch {
 constexpr size_t kScratchSets = 8;
 static std::mutex g_srbd_scratch_mu;
 static std::map<std::pair<int, hipStream_t>, SrbdScratch> g_srbd_scratch;
+static std::mutex g_srbd_pinned_mu;        // guards g_srbd_pinned (released sets push to it unlocked)
 static std::vector<void *> g_srbd_pinned;  // memory a captured graph may still read
 static uint64_t g_srbd_tick = 0;
 
+// Releases a set that is no longer in g_srbd_scratch (the caller does not
+// hold g_srbd_scratch_mu: the wait for the set's last launch blocks no other
+// thread's class dispatch).  The calls run in this thread's relaxed capture
+// mode, so a stream capture another thread runs in global mode
+// (torch.cuda.graph's default) is not invalidated by them (INTEGRATION.md,
+// graph capture).
 static void srbd_release(SrbdScratch &s) {
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
   if (s.done_recorded) (void)hipEventSynchronize(s.done);
   for (int k = 0; k < 3; ++k) {
     if (s.side[k]) (void)hipStreamDestroy(s.side[k]);
@@ -1381,27 +1390,34 @@ static void srbd_release(SrbdScratch &s) {
   if (s.fork) (void)hipEventDestroy(s.fork);
   if (s.done) (void)hipEventDestroy(s.done);
   if (s.captured) {
+    std::lock_guard<std::mutex> lk(g_srbd_pinned_mu);
     g_srbd_pinned.push_back(s.lists);
     g_srbd_pinned.push_back(s.counts);
   } else {
     if (s.lists) (void)hipFree(s.lists);
     if (s.counts) (void)hipFree(s.counts);
   }
+  if (swapped) (void)hipThreadExchangeStreamCaptureMode(&mode);
   s = SrbdScratch();
 }
 
 // Live scratch sets and pinned allocations (tests: the bound holds).
 extern "C" int qloco_srbd_scratch_sets(int32_t *pinned) {
   std::lock_guard<std::mutex> lk(g_srbd_scratch_mu);
-  if (pinned) *pinned = (int32_t)g_srbd_pinned.size();
+  if (pinned) {
+    std::lock_guard<std::mutex> lp(g_srbd_pinned_mu);
+    *pinned = (int32_t)g_srbd_pinned.size();
+  }
   return (int)g_srbd_scratch.size();
 }
 
 // Caller holds g_srbd_scratch_mu for the whole enqueue sequence (counter
 // reset, classification, class launches, the done event): two threads
 // sharing one stream must not interleave their sequences on the shared
-// counters.
-static int srbd_scratch(int64_t batch, hipStream_t st, bool capturing, SrbdScratch **out) {
+// counters.  A least-recently-used set evicted to make room is moved out of
+// the map into *victim; the caller releases it after dropping the lock.
+static int srbd_scratch(int64_t batch, hipStream_t st, bool capturing, SrbdScratch **out,
+                        SrbdScratch *victim) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return QLOCO_ERR_DEVICE;
   const auto key = std::make_pair(dev, st);
@@ -1413,26 +1429,32 @@ static int srbd_scratch(int64_t batch, hipStream_t st, bool capturing, SrbdScrat
                      hipErrorStreamCaptureUnsupported);
       return QLOCO_ERR_ARG;
     }
-    // bound the live sets: release the least recently used one first
+    // a new set is built completely before it enters the map: a failure part
+    // way leaves nothing half-initialised behind (the next call retries)
+    SrbdScratch fresh;
+    bool ok = hipMalloc(&fresh.counts, 8 * sizeof(int)) == hipSuccess;
+    for (int k = 0; ok && k < 3; ++k) {
+      ok = hipStreamCreateWithFlags(&fresh.side[k], hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&fresh.join[k], hipEventDisableTiming) == hipSuccess;
+    }
+    ok = ok && hipEventCreateWithFlags(&fresh.fork, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&fresh.done, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      srbd_release(fresh);
+      return QLOCO_ERR_DEVICE;
+    }
+    // bound the live sets: the least recently used one leaves the map (the
+    // caller releases it after unlocking)
     if (g_srbd_scratch.size() >= kScratchSets) {
       auto lru = g_srbd_scratch.begin();
       for (auto j = g_srbd_scratch.begin(); j != g_srbd_scratch.end(); ++j)
         if (j->second.last_use < lru->second.last_use) lru = j;
-      srbd_release(lru->second);
+      *victim = lru->second;
       g_srbd_scratch.erase(lru);
     }
-    it = g_srbd_scratch.emplace(key, SrbdScratch()).first;
+    it = g_srbd_scratch.emplace(key, fresh).first;
   }
   SrbdScratch &s = it->second;
-  if (!s.counts) {
-    if (hipMalloc(&s.counts, 8 * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
-    for (int k = 0; k < 3; ++k) {
-      if (hipStreamCreateWithFlags(&s.side[k], hipStreamNonBlocking) != hipSuccess) return QLOCO_ERR_DEVICE;
-      if (hipEventCreateWithFlags(&s.join[k], hipEventDisableTiming) != hipSuccess) return QLOCO_ERR_DEVICE;
-    }
-    if (hipEventCreateWithFlags(&s.fork, hipEventDisableTiming) != hipSuccess) return QLOCO_ERR_DEVICE;
-    if (hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return QLOCO_ERR_DEVICE;
-  }
   if (batch > s.cap) {
     if (capturing) {
       set_last_error("qloco_srbd_solve_ex: class-dispatch scratch must be sized before stream "
@@ -1445,6 +1467,7 @@ static int srbd_scratch(int64_t batch, hipStream_t st, bool capturing, SrbdScrat
     if (hipMalloc(&lists, kSrbdClasses * cap * sizeof(int)) != hipSuccess) return QLOCO_ERR_DEVICE;
     if (s.lists) {
       if (s.captured) {
+        std::lock_guard<std::mutex> lp(g_srbd_pinned_mu);
         g_srbd_pinned.push_back(s.lists);  // a graph may still read the old lists
       } else {
         // every earlier use was enqueued on this stream
@@ -1582,9 +1605,9 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
     }
   };
   const int top = srbd_class_of(legs, ws);
-  if (a.literal && a.N <= kLitN && !a.feet_per_step) {
-    // the literal QP at N <= 10: one wave per instance through the wrench
-    // space (qloco_srbd_lit.inc)
+  if (a.literal && a.N <= kLitN2 && !a.feet_per_step) {
+    // the literal QP at N <= 20 through the wrench space: one wave per
+    // instance for N <= 10, two for 11..20 (qloco_srbd_lit.hip)
     const int rc = srbd_lit_launch(a, ws, st);
     if (rc != QLOCO_OK) return rc;
   } else if (top == 0 || a.literal) {
@@ -1592,12 +1615,22 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
     // classification and no empty class launches
     launch(top, st);
   } else {
-    std::lock_guard<std::mutex> lk(g_srbd_scratch_mu);
+    std::unique_lock<std::mutex> lk(g_srbd_scratch_mu);
     hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
     const bool capturing =
         hipStreamIsCapturing(st, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone;
     SrbdScratch *sc = nullptr;
-    const int rc = srbd_scratch(batch, st, capturing, &sc);
+    SrbdScratch victim;
+    // an evicted set is released after the lock is dropped, whatever the exit
+    struct ReleaseAfterUnlock {
+      std::unique_lock<std::mutex> &lk;
+      SrbdScratch &v;
+      ~ReleaseAfterUnlock() {
+        if (lk.owns_lock()) lk.unlock();
+        if (v.counts || v.lists) srbd_release(v);
+      }
+    } release_victim{lk, victim};
+    const int rc = srbd_scratch(batch, st, capturing, &sc, &victim);
     if (rc != QLOCO_OK) return rc;
     QLOCO_HIP_CHECK(hipMemsetAsync(sc->counts, 0, 8 * sizeof(int), st), "class counters");
     hipLaunchKernelGGL(srbd_classify_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st,

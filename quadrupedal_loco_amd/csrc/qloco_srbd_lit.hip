@@ -1,8 +1,9 @@
 // qloco_srbd_lit.hip -- the reference's LITERAL 12N-variable SRBD QP for
-// N <= 10 (every (step, leg) pair an ADMM variable, swing legs held by their
+// N <= 20 (every (step, leg) pair an ADMM variable, swing legs held by their
 // fz in [0, 0] rows: A1RobotControl.cpp:557-578, ConvexMpc.cpp:162-264),
-// one wavefront per instance, the OSQP linear solve through the per-step
-// wrench space (dispatched by qloco_srbd_solve_ex, qloco_srbd.hip).
+// the OSQP linear solve through the per-step wrench space, one wavefront per
+// instance for N <= 10 and two for 11 <= N <= 20 (dispatched by
+// qloco_srbd_solve_ex, qloco_srbd.hip).
 //
 // Why the wrench space.  The forces enter the SRBD dynamics
 // only through each step's wrench increment w_j = Bb u_j (Bb: the omega / v
@@ -15,19 +16,26 @@
 //   K^-1 b = D^-1 (a - W0^-1 Vu' T Vu a),  a = W0^-1 D^-1 b,
 //   T = (I + cG U)^-1 cG = (cG) L S^-1 L^-1   (symmetric, 6N x 6N),
 //   U = Vu W0^-1 Vu' = L L' (6 x 6 per step),  S = I + L' (cG) L  (SPD, >= I).
-// The 120-variable KKT inverse of the two-wave kernel (a 120 x 120 Gauss-
-// Jordan, 2 x 124 register columns per lane) becomes a 60 x 60 inverse of the
+// The 12N-variable KKT inverse becomes a 6N x 6N inverse of the
 // well-conditioned S (eigenvalues >= 1, so pivot-free Gauss-Jordan is
-// stable) plus a 60 x 60 product, and each ADMM iteration a 60 x 60 matvec
-// plus leg-local 3 x 3 blocks and per-step wrench sums -- one wave, 60
-// register columns.  Same arithmetic as OSQP up to rounding
-// (tools/proto_lit.py: float64 iterates agree to 1e-10, a float32 solve to
-// 4e-7 relative; iteration counts equal on every instance tried).
+// stable) plus a 6N x 6N product, and each ADMM iteration a 6N x 6N matvec
+// plus leg-local 3 x 3 blocks and per-step wrench sums.  Same arithmetic as
+// OSQP up to rounding (tools/proto_lit.py: float64 iterates agree to 1e-10,
+// a float32 solve to 4e-7 relative; iteration counts equal on every instance
+// tried).
 //
-// Lane l holds two variables (slot h = 0, 1: v = 60 h + l, l < 60; step
-// v / 12, leg (v % 12) / 3, component v % 3 -- leg triples never straddle),
-// their <= 2 constraint rows each (as the two-wave kernel), and wrench row
-// r = l (step l / 6, component l % 6: 0..2 omega, 3..5 v).
+// Lane layout (template W = waves per instance).  Wave w holds the steps
+// [w H, w H + N_w) (W = 1: H = N_0 = N; W = 2: H = ceil(N / 2), N_1 = N - H,
+// at most 10 steps a wave), laid out exactly as the one-wave kernel lays out
+// its N <= 10 steps: lane l holds two variables (slot h = 0, 1: local
+// v = 60 h + l, l < 60; step w H + v / 12, leg (v % 12) / 3, component
+// v % 3 -- leg triples never straddle), their <= 2 constraint rows each,
+// and wrench row l (step w H + l / 6, component l % 6: 0..2 omega, 3..5 v).
+// Everything leg- or step-local stays inside a wave; the couplings across
+// steps (the K0 / K2 horizon sums, the rows of S and T, the matvec with T)
+// run in a "column space" of W halves of 60 (half w' = wave w''s wrench rows),
+// so a lane's row of S / T is 60 W registers and the Gauss-Jordan and the
+// matvec are W of the one-wave kernel's 60-column DPP forms.
 #include <math.h>
 
 #include <type_traits>
@@ -36,44 +44,57 @@
 
 namespace qloco {
 
-constexpr int kLitWpe = 4;  // waves per SIMD: 128 VGPRs, <= 10 KB of LDS (static_assert below)
+constexpr int kLitWpe = 4;   // one wave:  waves per SIMD: 128 VGPRs, <= 10 KB of LDS (static_assert below)
+constexpr int kLit2Wpe = 2;  // two waves: 256 VGPRs (a 120-register row of S / T per lane)
 
+template <int W>
 struct LitLds {
-  f4v bc[16];               // broadcast row: 60-vectors read as one 16-B chunk per lane (one
-                            // wave: its LDS ops run in order, so one buffer serves every reuse)
-  float av[2][64];          // per-slot exchange (a, D x, t)
-  float wv[64];             // wrench rows (s, w)
-  f2v k0k2[kLitN][kLitN];   // horizon sums K0 / K2 (row step, column step)
+  // steps the per-step loops unroll over; the per-step tables (K0 / K2, L_j,
+  // L_j^-1, Ruiz column scales) are indexed by COLUMN-SPACE step 10 w' + kl
+  // (wave w''s local step kl; two waves: the steps past a wave's N_w are
+  // padding with zero K0 / K2 weights), so every table index in the unrolled
+  // loops is a compile-time constant plus the wave's offset
+  static constexpr int NS = W == 1 ? kLitN : kLitN2;
+  static constexpr int NT = NS;
+  f4v bc[W][W][16];         // broadcast rows: 60-vectors read as one 16-B chunk per lane, [parity][half]
+                            // (one wave: its LDS ops run in order, so one buffer serves every reuse;
+                            // two waves: double-buffered by iteration / pivot parity, one barrier each)
+  float av[W][2][64];       // per wave, per slot exchange (a, D x, t)
+  float wv[W][64];          // per wave, wrench rows (s, w)
+  f2v k0k2[NT][NT];         // horizon sums K0 / K2 (row step, column step; column-space steps)
   float Bb[6][12];          // wrench map (constant feet), rows omega 0..2, v 3..5
   float Te[6][6];           // dt^2 blockdiag(Rz' Qtheta Rz, Qp)
   float q2[16], r2[12], x0[16];
-  float ctf[4 * kLitN];     // contact flags as floats
-  f4v arz[2][64];           // per slot: scaled A entries (ra0, ra1, rz0, rz1)
-  float zh[2][64];          // per slot: row 0's scaled upper bound (x / y rows: inf); the lower
+  float ctf[4 * NT];        // contact flags as floats
+  f4v arz[W][2][64];        // per slot: scaled A entries (ra0, ra1, rz0, rz1)
+  float zh[W][2][64];       // per slot: row 0's scaled upper bound (x / y rows: inf); the lower
                             // bound is 0 (x / y) or zh fz_min / fz_max (z rows)
-  union {                   // phase-local storage (LDS bounds the occupancy: <= 20 KB)
+  union {                   // phase-local storage (LDS bounds the one-wave occupancy: <= 10 KB)
     struct {                // gradient + Ruiz
       f2v beps[12][12];     // (beta, eps)[w][w']: the P entries' per-column coefficients
-      float dcol[120];      // Ruiz column scales D (read as same-address broadcasts)
-      float err[12 * kLitN];  // gradient scans
-      float Wc[12 * kLitN];
+      float dcol[12 * NT];  // Ruiz column scales D (read as same-address broadcasts)
+      float err[12 * NT];   // gradient scans
+      float Wc[12 * NT];
     };
     struct {                // factorisation
-      float Lt[kLitN][21];    // per step: columns of L_j, packed (column t: rows t..5 at tri(t))
-      float Li[kLitN][21];    // per step: columns of L_j^-1, packed the same way
+      float Lt[NT][21];     // per step: columns of L_j, packed (column t: rows t..5 at tri(t))
+      float Li[NT][21];     // per step: columns of L_j^-1, packed the same way
       union {
         struct {
-          float w0i[3][2][64];     // per variable: its row of W0^-1 (x, y, z), until the U rows
-          float U[kLitN][6][6];    // per step: U_j (until its Cholesky)
+          float w0i[W][3][2][64];   // per variable: its row of W0^-1 (x, y, z), until the U rows
+          float U[W][kLitN][6][6];  // per step: U_j (until its Cholesky)
         };
         struct {
-          f4v zc[64], tc[64];  // T passes: Z (then L Z, same wave, in order), Te L Z columns
-        };
+          f4v zc[W][W][64], tc[W][W][64];  // T passes: Z (then L Z, same wave, in order), Te L Z
+        };                                 // columns, [parity][wave]
       };
     };
   };
+  float piv[W == 1 ? 0 : 2];       // two waves: the Gauss-Jordan pivot, [parity]
+  float red[W == 1 ? 0 : 2][16];   // two waves: per-wave partials of the block reductions
 };
-static_assert(sizeof(LitLds) <= 10240, "literal kernel: four workgroups per SIMD need <= 160 KB / 16 of LDS");
+static_assert(sizeof(LitLds<1>) <= 10240, "literal kernel: four workgroups per SIMD need <= 160 KB / 16 of LDS");
+static_assert(sizeof(LitLds<2>) <= 40960, "two-wave literal kernel: four workgroups per CU need <= 40 KB");
 
 // Packed lower-triangular 6 x 6 columns: column t (rows t..5) starts at
 // tri(t); tri(t) - t + s addresses row s >= t.
@@ -84,6 +105,47 @@ __device__ __forceinline__ void lsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// the instance's workgroup: a wave barrier for one wave, s_barrier for two
+template <int W>
+__device__ __forceinline__ void bsync() {
+  if constexpr (W == 1)
+    lsync();
+  else
+    __syncthreads();
+}
+
+// Block-wide combination of W wave-uniform partials (fixed order: every wave
+// computes the same value bit for bit, so the loop control stays uniform)
+template <int W, int K>
+__device__ __forceinline__ void bcombine_max(LitLds<W> &S, float (&v)[K], int wv) {
+  if constexpr (W == 2) {
+    static_assert(K <= 16, "red holds 16 partials per wave");
+    if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) S.red[wv][k] = v[k];
+    }
+    bsync<W>();
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = fmaxf(S.red[0][k], S.red[1][k]);
+    bsync<W>();
+  }
+}
+template <int W>
+__device__ __forceinline__ float bsum(LitLds<W> &S, float v, int wv) {
+  if constexpr (W == 2) {
+    if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) S.red[wv][0] = v;
+    bsync<W>();
+    v = S.red[0][0] + S.red[1][0];
+    bsync<W>();
+  }
+  return v;
+}
+template <int W>
+__device__ __forceinline__ float bmax1(LitLds<W> &S, float v, int wv) {
+  float t[1] = {v};
+  bcombine_max<W, 1>(S, t, wv);
+  return t[0];
 }
 
 // The three entries of this lane's leg triple (components 0, 1, 2) of a
@@ -138,12 +200,12 @@ __device__ __forceinline__ float tdot(float v, const Shift5 &c) {
 // column k + 1 alone (the same fused multiply-add the full update performs,
 // so bit-identical) and publishes pivot k + 1's broadcast row, then runs the
 // other 59 columns while that LDS write is in flight.
-__device__ __forceinline__ void lit_invert(LitLds &S, int lane, int ncol, Row<1> &K) {
+__device__ __forceinline__ void lit_invert(LitLds<1> &S, int lane, int ncol, Row<1> &K) {
   int nc = __builtin_amdgcn_readfirstlane(ncol);
   {
     const float v = K.k[0];
     const float p = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
-    reinterpret_cast<float *>(&S.bc[0])[lane] = lane == 0 ? p + 1.0f : v;
+    reinterpret_cast<float *>(&S.bc[0][0][0])[lane] = lane == 0 ? p + 1.0f : v;
   }
   ColLoop<0, 60>::run([&](auto kc) {
     constexpr int k = decltype(kc)::value;
@@ -151,7 +213,7 @@ __device__ __forceinline__ void lit_invert(LitLds &S, int lane, int ncol, Row<1>
     if (k >= nc) return;
     const int tt = fresh_lane();
     lsync();
-    const f4v r0 = S.bc[lane & 15];
+    const f4v r0 = S.bc[0][0][lane & 15];
     const float v = K.k[k];
     const float p = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
     const float pinv = __builtin_amdgcn_rcpf(p);
@@ -159,12 +221,81 @@ __device__ __forceinline__ void lit_invert(LitLds &S, int lane, int ncol, Row<1>
     if constexpr (k + 1 < 60) {  // unconditional (harmless past the last pivot): no branch to join
       const float la = fmaf(dpp_col<k + 1>(r0), ng, K.k[k + 1]);
       const float p1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, la), k + 1));
-      reinterpret_cast<float *>(&S.bc[0])[tt] = (tt == k + 1) ? p1 + 1.0f : ((tt < k + 1) ? -la : la);
+      reinterpret_cast<float *>(&S.bc[0][0][0])[tt] = (tt == k + 1) ? p1 + 1.0f : ((tt < k + 1) ? -la : la);
     }
     QL_DPP_GJ60(K.k, 0, r0, ng);
     if (p > kGjExactPivot) K.k[k] = (tt == k) ? pinv : ng;
   });
   lsync();
+}
+
+// The two-wave form: S is (60 + 60) x (60 + 60) in column space (wave w's
+// rows are rows 60 w .. 60 w + 59, its first nc_w valid), one row of 120
+// registers per lane.  Each pivot publishes its column (the pivot row up to
+// the Gauss-Jordan signs) from both waves into the parity buffer, one
+// workgroup barrier, then both halves take the one-wave DPP update.  The
+// look-ahead publishes the next pivot's column before the 120-column update,
+// so the barrier never waits on that write; the pivot value itself travels
+// through LDS (the other wave cannot read the owner's register).
+//
+// Pivot order: LAST step first (half 1 from its last valid row down, then
+// half 0).  S's early steps carry the largest horizon weights (K0 = N - j,
+// K2 ~ (N - j)^3 / 3): eliminating them first, as the one-wave kernel's
+// natural order does, grows the error of the pivot-free fp32 Gauss-Jordan
+// past what ADMM tolerates at N = 16 / 20 and small rho (57 + 4 of 65,536
+// N = 16 trot instances ended at max_iter / solved-inaccurate; the float32
+// emulation, tools/proto_lit_fused.py, reproduces it and converges with the
+// reversed order on every one of them).
+template <int HF, int KL>
+__device__ __forceinline__ void lit2_pivot(LitLds<2> &S, int wv, int nc, Row<2> &K) {
+  const int tt = fresh_lane();
+  if constexpr (KL >= 1) {
+    if (KL == nc) {  // the half's first pivot (column KL - 1): a plain publish
+      constexpr int k1 = 60 * HF + KL - 1;
+      const float v = K.k[k1];
+      const bool own1 = wv == HF && tt == KL - 1;
+      const bool before = HF == 0 && wv == 1;  // half 1 is done when half 0 starts
+      reinterpret_cast<float *>(&S.bc[k1 & 1][wv][0])[tt] = own1 ? v + 1.0f : (before ? -v : v);
+      if (own1) S.piv[k1 & 1] = v;
+    }
+  }
+  if constexpr (KL < 60) {
+    constexpr int k = 60 * HF + KL;
+    constexpr int pb = k & 1;
+    if (KL >= nc) return;
+    bsync<2>();
+    const f4v r0 = S.bc[pb][0][tt & 15];
+    const f4v r1 = S.bc[pb][1][tt & 15];
+    const float p = S.piv[pb];
+    const float v = K.k[k];
+    const float pinv = __builtin_amdgcn_rcpf(p);
+    const bool own = wv == HF && tt == KL;
+    const float ng = -(own ? (1.0f - pinv) : v * pinv);
+    if constexpr (KL >= 1) {  // look-ahead: the next pivot is column k - 1 of this half
+      const float la = fmaf(dpp_col<KL - 1>(HF ? r1 : r0), ng, K.k[k - 1]);
+      const bool own1 = wv == HF && tt == KL - 1;
+      const bool before = HF ? (wv == 1 && tt >= KL) : (wv == 1 || tt >= KL);
+      reinterpret_cast<float *>(&S.bc[pb ^ 1][wv][0])[tt] = own1 ? la + 1.0f : (before ? -la : la);
+      if (own1) S.piv[pb ^ 1] = la;
+    }
+    QL_DPP_GJ60(K.k, 0, r0, ng);
+    QL_DPP_GJ60(K.k, 60, r1, ng);
+    if (p > kGjExactPivot) K.k[k] = own ? pinv : ng;
+  }
+}
+
+__device__ __forceinline__ void lit_invert2(LitLds<2> &S, int wv, int nc0, int nc1, Row<2> &K) {
+  nc0 = __builtin_amdgcn_readfirstlane(nc0);
+  nc1 = __builtin_amdgcn_readfirstlane(nc1);
+  ColLoop<0, 61>::run([&](auto kc) {  // half 1, KL = 60 .. 0
+    asm volatile("" : "+s"(nc1));
+    lit2_pivot<1, 60 - decltype(kc)::value>(S, wv, nc1, K);
+  });
+  ColLoop<0, 61>::run([&](auto kc) {  // half 0
+    asm volatile("" : "+s"(nc0));
+    lit2_pivot<0, 60 - decltype(kc)::value>(S, wv, nc0, K);
+  });
+  bsync<2>();
 }
 
 // 6 x 6 Cholesky L L' = A (lower, row-major a[r][c]) and L^-1, all in
@@ -206,32 +337,45 @@ __device__ __forceinline__ void chol6(const float (&a)[6][6], float (&L)[6][6], 
 // Lane-derived indices re-derived from an opaque copy of the lane at the top
 // of a phase: the address arithmetic on them is then recomputed there (a few
 // VALU) instead of hoisted to the kernel entry and kept live -- at 128 VGPRs
-// the hoisted offsets were the setup's scratch spills.
+// the hoisted offsets were the setup's scratch spills.  jr / stepl: the
+// wave-local step (per-wave LDS rows); step: the global step (the
+// gradient, the contact flags, the persistent record); jc: the column-space
+// step (the horizon tables: 10 w + jr).  Padding lanes sit on steps whose
+// K0 / K2 weights are zero.
 #define QL_LIT_LANE_INDICES(LX)                                                                    \
   const int LX = fresh_lane();                                                                     \
   const int jr = LX < 60 ? LX / 6 : kLitN - 1, sr = LX < 60 ? LX - 6 * (LX / 6) : 0;               \
+  const int jc = W == 1 ? jr : 10 * wv + jr;                                                       \
   const bool wvalid = LX < nw;                                                                     \
-  const int step[2] = {LX < 60 && LX < nvar ? LX / 12 : 0, LX < 60 && 60 + LX < nvar ? (60 + LX) / 12 : 0}; \
-  const int leg[2] = {LX < 60 && LX < nvar ? (LX % 12) / 3 : 0, LX < 60 && 60 + LX < nvar ? ((60 + LX) % 12) / 3 : 0}; \
+  const int step[2] = {LX < 60 && LX < nvl ? so + LX / 12 : so, LX < 60 && 60 + LX < nvl ? so + (60 + LX) / 12 : so}; \
+  const int stepl[2] = {step[0] - so, step[1] - so};                                               \
+  const int leg[2] = {LX < 60 && LX < nvl ? (LX % 12) / 3 : 0, LX < 60 && 60 + LX < nvl ? ((60 + LX) % 12) / 3 : 0}; \
   const int comp = LX % 3;                                                                         \
   const bool xy = comp < 2;                                                                        \
-  const bool valid[2] = {LX < 60 && LX < nvar, LX < 60 && 60 + LX < nvar};                         \
-  (void)jr; (void)sr; (void)wvalid; (void)step; (void)leg; (void)comp; (void)xy; (void)valid
+  const bool valid[2] = {LX < 60 && LX < nvl, LX < 60 && 60 + LX < nvl};                           \
+  (void)jr; (void)sr; (void)jc; (void)wvalid; (void)stepl; (void)step; (void)leg; (void)comp; (void)xy; (void)valid
 
 // WS: a warm-start mode (1 or 2) may be set (the persistent record of
 // DESIGN.md §3c, literal semantics: the update path on every call).
-template <bool WS>
-__device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const int64_t b) {
-  const int lane = threadIdx.x;
+template <int W, bool WS>
+__device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, const int64_t b) {
+  constexpr int NS = LitLds<W>::NS, NT = LitLds<W>::NT;
+  const int lane = W == 1 ? (int)threadIdx.x : (int)(threadIdx.x & 63);
+  const int tid = threadIdx.x;
+  const int wv = W == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int N = a.N;
   const float Nf = (float)N;
   const float dt = a.dt;
   const float dtm = dt / a.mass, dt2m = dt * dt / a.mass;
-  const int nvar = 12 * N, nw = 6 * N;
+  // this wave's steps: [so, so + Nw) (W = 1: all N)
+  const int H = W == 1 ? N : (N + 1) / 2;
+  const int so = W == 1 ? 0 : wv * H;
+  const int Nw = W == 1 ? N : (wv ? N - H : H);
+  const int nvar = 12 * N, nvl = 12 * Nw, nw = 6 * Nw;
 
   // ---------------- 1. inputs -> LDS
-  if (lane < 13) S.x0[lane] = a.x0[b * 13 + lane];
-  if (lane == 0) {
+  if (tid < 13) S.x0[tid] = a.x0[b * 13 + tid];
+  if (tid == 0) {
 #pragma unroll
     for (int k = 0; k < 13; ++k) S.q2[k] = a.q2[k];
 #pragma unroll
@@ -239,15 +383,24 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   }
   {
     const int nct = a.contacts_per_step ? 4 * N : 4;
-    if (lane < 4 * N) S.ctf[lane] = a.contacts[b * nct + (a.contacts_per_step ? lane : (lane & 3))] ? 1.0f : 0.0f;
+    if (tid < 4 * N) S.ctf[tid] = a.contacts[b * nct + (a.contacts_per_step ? tid : (tid & 3))] ? 1.0f : 0.0f;
   }
-  for (int idx = lane; idx < kLitN * kLitN; idx += 64) {
-    const int sr = idx / kLitN, sc = idx - kLitN * sr;
+  for (int idx = tid; idx < NT * NT; idx += 64 * W) {
+    const int sr = idx / NT, sc = idx - NT * sr;
     float K0 = 0.0f, K2 = 0.0f;
-    if (sr < N && sc < N) k0k2((float)sr, (float)sc, Nf, K0, K2);
+    if constexpr (W == 1) {
+      if (sr < N && sc < N) k0k2((float)sr, (float)sc, Nf, K0, K2);
+    } else {  // column-space steps -> global steps (-1: padding)
+      const int gr = sr % 10 < (sr >= 10 ? N - H : H) ? (sr >= 10 ? H : 0) + sr % 10 : -1;
+      const int gc = sc % 10 < (sc >= 10 ? N - H : H) ? (sc >= 10 ? H : 0) + sc % 10 : -1;
+      if (gr >= 0 && gc >= 0) k0k2((float)gr, (float)gc, Nf, K0, K2);
+    }
     S.k0k2[sr][sc] = (f2v){K0, K2};
   }
-  lsync();
+  if constexpr (W == 2) {  // Ruiz column scales of the padding steps stay 0
+    for (int idx = tid; idx < 12 * NT; idx += 64 * W) S.dcol[idx] = 0.0f;
+  }
+  bsync<W>();
 
   // ---------------- 2. SRBD model (ConvexMpc.cpp:111-160, compute_grf :502-549)
   const float yaw = S.x0[2];
@@ -286,13 +439,14 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   const int comp = lane % 3;
   const bool xy = comp < 2;
   bool valid[2];
-  int step[2], leg[2];
+  int step[2], leg[2], cst[2];  // global / column-space step
   f4v lo[2], hi[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int v = 60 * h + lane;
-    valid[h] = lane < 60 && v < nvar;
-    step[h] = valid[h] ? v / 12 : 0;
+    valid[h] = lane < 60 && v < nvl;
+    step[h] = valid[h] ? so + v / 12 : 0;
+    cst[h] = W == 1 ? step[h] : (valid[h] ? 10 * wv + v / 12 : 0);
     leg[h] = valid[h] ? (v % 12) / 3 : 0;
     const float *rf = a.feet + b * 12 + 3 * leg[h];
     const float rx = rf[0], ry = rf[1], rz = rf[2];
@@ -309,7 +463,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       hi[h] = (f4v){0.0f, 0.0f, 0.0f, -1.0f};
     }
     // the wrench map (constant feet): column v % 12 of Bb from the step-0 lanes
-    if (h == 0 && lane < 12) {
+    if (h == 0 && tid < 12) {
       S.Bb[0][lane] = ba[0];
       S.Bb[1][lane] = ba[1];
       S.Bb[2][lane] = ba[2];
@@ -319,7 +473,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     }
   }
   // Te = dt^2 blockdiag(Rz' diag(q2[0:3]) Rz, diag(q2[3:6]))
-  if (lane < 36) {
+  if (tid < 36) {
     const int r = lane / 6, c = lane - 6 * (lane / 6);
     const float Rm[3][3] = {{R00, R01, 0.f}, {R10, R11, 0.f}, {0.f, 0.f, 1.f}};
     float v = 0.0f;
@@ -334,7 +488,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   for (int h = 0; h < 2; ++h) r2v[h] = valid[h] ? S.r2[3 * leg[h] + comp] : 0.0f;
 
   // ---------------- 3. gradient g = Bqp' Q (Aqp x0 - x_ref) (ConvexMpc.cpp:219-221)
-  for (int idx = lane; idx < 12 * N; idx += 64) {
+  for (int idx = tid; idx < 12 * N; idx += 64 * W) {
     const int i = idx / 12, s = idx - 12 * i;
     const float k = (float)(i + 1);
     const float *x0 = S.x0;
@@ -352,13 +506,13 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     }
     S.err[idx] = S.q2[s] * (xf - a.xref[b * 13 * N + 13 * i + s]);
   }
-  lsync();
-  if (lane < 12) {  // suffix scans per state row (row_scans of the two-wave kernel)
+  bsync<W>();
+  if (tid < 12) {  // suffix scans per state row (row_scans of the two-wave kernel)
     const int r = lane;
     const bool brow = r >= 6;
     float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
-    for (int j = kLitN - 1; j >= 0; --j) {
+    for (int j = NS - 1; j >= 0; --j) {
       if (j < N) {
         s1 += s0;
         s0 += S.err[12 * j + r];
@@ -366,7 +520,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       }
     }
   }
-  lsync();
+  bsync<W>();
   float qv[2], qsv[2], q_raw[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -416,8 +570,8 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   {
     // beta / eps tables (12 x 12, constant feet) in LDS: beta[w][w'] =
     // sum_s Qb_s Bb[s][w] Bb[s][w'], eps[w][w'] = Bb[:,w]' Te Bb[:,w']
-    lsync();
-    for (int e = lane; e < 144; e += 64) {
+    bsync<W>();
+    for (int e = tid; e < 144; e += 64 * W) {
       const int w = e / 12, wp = e - 12 * (e / 12);
       float bb = 0.0f, ee = 0.0f;
 #pragma unroll
@@ -430,13 +584,13 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       }
       S.beps[w][wp] = (f2v){bb, ee};
     }
-    lsync();
+    bsync<W>();
     // this lane's diagonal P entries (R included)
     float pdiag[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int wl = valid[h] ? (60 * h + lane) % 12 : 0;
-      const f2v kk = S.k0k2[step[h]][step[h]];
+      const f2v kk = S.k0k2[cst[h]][cst[h]];
       const f2v be = S.beps[wl][wl];
       pdiag[h] = valid[h] ? fmaf(kk.y, be.y, kk.x * be.x) + r2v[h] : 0.0f;
     }
@@ -453,7 +607,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         eps[h][w] = valid[h] ? be.y : 0.0f;
       }
     }
-    // row inf-norms |P_vc| D_c of both slots' rows in one sweep over the 120
+    // row inf-norms |P_vc| D_c of both slots' rows in one sweep over the 12N
     // columns, step-major: per column step the K0 / K2 weights of the two
     // rows' steps and the step's 12 column scales (same-address LDS reads,
     // a broadcast), then 12 entries per row from the (beta, eps) rows
@@ -468,15 +622,15 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       // arithmetic (one step of look-ahead, no more: all ten would be live)
       f2v ma = (f2v)(0.0f), mb = (f2v)(0.0f);
       const f4v one4 = (f4v)(1.0f);
-      f2v k0 = S.k0k2[step[0]][0], k1 = S.k0k2[step[1]][0];
+      f2v k0 = S.k0k2[cst[0]][0], k1 = S.k0k2[cst[1]][0];
       f4v da = scaled ? reinterpret_cast<const f4v *>(&S.dcol[0])[0] : one4,
           db = scaled ? reinterpret_cast<const f4v *>(&S.dcol[0])[1] : one4,
           dd = scaled ? reinterpret_cast<const f4v *>(&S.dcol[0])[2] : one4;
 #pragma unroll
-      for (int kc = 0; kc < kLitN; ++kc) {
-        const int kn = kc + 1 < kLitN ? kc + 1 : kc;
+      for (int kc = 0; kc < NS; ++kc) {
+        const int kn = kc + 1 < NS ? kc + 1 : kc;
         asm volatile("" ::: "memory");  // table reads stay in the pass (no LICM)
-        const f2v k0n = S.k0k2[step[0]][kn], k1n = S.k0k2[step[1]][kn];
+        const f2v k0n = S.k0k2[cst[0]][kn], k1n = S.k0k2[cst[1]][kn];
         const f4v *dcn = reinterpret_cast<const f4v *>(&S.dcol[12 * kn]);
         const f4v dan = scaled ? dcn[0] : one4, dbn = scaled ? dcn[1] : one4, ddn = scaled ? dcn[2] : one4;
         __builtin_amdgcn_sched_barrier(0);
@@ -533,16 +687,20 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         qv[h] *= Dt[h];
         qsv[h] *= Dt[h];
         Dr[h] *= Dt[h];
-        if (lane < 60) S.dcol[60 * h + lane] = valid[h] ? Dr[h] : 0.0f;
+        if constexpr (W == 1) {
+          if (lane < 60) S.dcol[60 * h + lane] = valid[h] ? Dr[h] : 0.0f;
+        } else {
+          if (valid[h]) S.dcol[120 * wv + 60 * h + lane] = Dr[h];  // column-space order
+        }
       }
-      lsync();
+      bsync<W>();
       float cn2[2], mr[2];
       row_norms(true, mr);
 #pragma unroll
       for (int h = 0; h < 2; ++h) cn2[h] = valid[h] ? Dr[h] * fmaxf(mr[h], pdiag[h] * Dr[h]) : 0.0f;
       // cost scaling: mean column norm of the scaled P vs ||q||_inf
-      const float sumP = wsum(cn2[0] + cn2[1]);
-      const float qm = wmax_nonneg(fmaxf(valid[0] ? fabsf(qsv[0]) : 0.0f, valid[1] ? fabsf(qsv[1]) : 0.0f));
+      const float sumP = bsum<W>(S, wsum(cn2[0] + cn2[1]), wv);
+      const float qm = bmax1<W>(S, wmax_nonneg(fmaxf(valid[0] ? fabsf(qsv[0]) : 0.0f, valid[1] ? fabsf(qsv[1]) : 0.0f)), wv);
       const float meanP = cs * sumP * inv_n;
       const float ctc = __builtin_amdgcn_rcpf(limit_scaling(fmaxf(meanP, limit_scaling(qm))));
 #pragma unroll
@@ -552,7 +710,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         cnP[h] = cn2[h] * cs * ctc;
       }
       cs *= ctc;
-      lsync();
+      bsync<W>();
     }
   }
   // block-uniform scalars live in SGPRs (a VGPR copy would be kept, and
@@ -565,19 +723,20 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   for (int h = 0; h < 2; ++h) {
     const float lh0 = rl0[h] * rE0[h], uh0 = ru0[h] * rE0[h];
     eq0[h] = valid[h] && !xy && (uh0 - lh0 < 1e-4f);  // OSQP set_rho_vec: RHO_TOL
-    S.zh[h][lane] = uh0;
-    S.arz[h][lane] = (f4v){ra0[h], ra1[h], rz0[h], rz1[h]};
+    S.zh[wv][h][lane] = uh0;
+    S.arz[wv][h][lane] = (f4v){ra0[h], ra1[h], rz0[h], rz1[h]};
     qn[0] = fmaxf(qn[0], valid[h] ? fabsf(qv[h] / Dr[h]) : 0.0f);
     qn[1] = fmaxf(qn[1], valid[h] ? fabsf(qv[h]) : 0.0f);
   }
   qn[0] = wmax_nonneg(qn[0]);
   qn[1] = wmax_nonneg(qn[1]);
+  bcombine_max<W, 2>(S, qn, wv);
   lsync();
 
   // row scaling E of a slot's two rows, from A~ = E A D (each row's entry in
   // its own variable's column is 1 before scaling)
   auto row_e = [&](int h) -> f2v {
-    const f4v arz = S.arz[h][fresh_lane()];
+    const f4v arz = S.arz[wv][h][fresh_lane()];
     const float d = Dr[h];
     return (f2v){valid[h] ? arz.x / d : 1.0f, (valid[h] && xy) ? arz.y / d : 1.0f};
   };
@@ -602,7 +761,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
                                                                : (a.adaptive_rho ? a.rho_interval : 0);
   int status = QLOCO_MAX_ITER, iter = 0, rho_updates = 0;
   float px[2] = {0.0f, 0.0f};
-  Row<1> T;        // T = (I + cG U)^-1 cG, this lane's wrench row
+  Row<W> T;        // T = (I + cG U)^-1 cG, this lane's wrench row (column space)
   Shift5 W1[2];  // per slot: this lane's row of W0^-1 as leg-triple shifts
   float Dinv[2];
 #pragma unroll
@@ -610,17 +769,18 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
 
   // P~ x (scaled) per slot: c D (Vu' G Vu + R) D x through the wrench rows
   auto p_times_x = [&](float (&out)[2]) {
+    if constexpr (W == 2) bsync<W>();  // the other wave is done with the iteration's broadcast rows
     QL_LIT_LANE_INDICES(lxp);
     float drp[2] = {Dr[0], Dr[1]};  // opaque: cs D is not hoisted into the loop-live set
     asm volatile("" : "+v"(drp[0]), "+v"(drp[1]));
 #pragma unroll
-    for (int h = 0; h < 2; ++h) S.av[h][lxp] = valid[h] ? x[h] * drp[h] : 0.0f;
+    for (int h = 0; h < 2; ++h) S.av[wv][h][lxp] = valid[h] ? x[h] * drp[h] : 0.0f;
     lsync();
     // w = Vu (D x): wrench row (jr, sr) sums its step's 12 variables
     float wr = 0.0f;
     {
       const int hh = jr >= 5 ? 1 : 0, base = 12 * (jr - 5 * hh);
-      const f4v *src = reinterpret_cast<const f4v *>(&S.av[hh][base]);
+      const f4v *src = reinterpret_cast<const f4v *>(&S.av[wv][hh][base]);
       const f4v u0 = src[0], u1 = src[1], u2 = src[2];
       const float uv[12] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w, u2.x, u2.y, u2.z, u2.w};
       const f4v *br = reinterpret_cast<const f4v *>(S.Bb[sr]);
@@ -630,38 +790,41 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       for (int w = 0; w < 12; ++w) wr = fmaf(bv[w], uv[w], wr);
       wr = wvalid ? wr : 0.0f;
     }
-    S.wv[lxp] = wr;
+    S.wv[wv][lxp] = wr;
     lsync();
     // Te w per row (needs the step's 6 wrench values)
     {
       float tw = 0.0f;
 #pragma unroll
-      for (int t = 0; t < 6; ++t) tw = fmaf(S.Te[sr][t], S.wv[6 * jr + t], tw);
-      reinterpret_cast<float *>(&S.bc[0])[lxp] = wvalid ? tw : 0.0f;  // Te w (bc is free in a check)
+      for (int t = 0; t < 6; ++t) tw = fmaf(S.Te[sr][t], S.wv[wv][6 * jr + t], tw);
+      reinterpret_cast<float *>(&S.bc[0][wv][0])[lxp] = wvalid ? tw : 0.0f;  // Te w (bc is free in a check)
     }
-    lsync();
+    bsync<W>();
     // (G w)[(jr, sr)] = Qb_s sum_k K0(jr,k) w(k,sr) + sum_k K2(jr,k) (Te w_k)_sr
     float gw = 0.0f;
     {
       const float qb = S.q2[6 + sr];
       float s0 = 0.0f, s2 = 0.0f;
 #pragma unroll
-      for (int k = 0; k < kLitN; ++k) {
-        const f2v kk = S.k0k2[jr][k];
-        s0 = fmaf(kk.x, S.wv[6 * k + sr], s0);
-        s2 = fmaf(kk.y, reinterpret_cast<const float *>(&S.bc[0])[6 * k + sr], s2);
+      for (int wp = 0; wp < W; ++wp) {
+#pragma unroll
+        for (int k = 0; k < kLitN; ++k) {
+          const f2v kk = S.k0k2[jc][10 * wp + k];
+          s0 = fmaf(kk.x, S.wv[wp][6 * k + sr], s0);
+          s2 = fmaf(kk.y, reinterpret_cast<const float *>(&S.bc[0][wp][0])[6 * k + sr], s2);
+        }
       }
       gw = wvalid ? fmaf(qb, s0, s2) : 0.0f;
     }
-    lsync();
-    S.wv[lxp] = gw;
+    bsync<W>();
+    S.wv[wv][lxp] = gw;
     lsync();
     // Vu' (G w) + R (D x), then c D (...)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       float acc = 0.0f;
       if (valid[h]) {
-        const float *gs = &S.wv[6 * step[h]];
+        const float *gs = &S.wv[wv][6 * stepl[h]];
         const int wc = lxp % 12;  // the variable's column of Bb (both slots: 60 = 5 x 12)
         acc = S.Bb[0][wc] * gs[0] + S.Bb[1][wc] * gs[1] + S.Bb[2][wc] * gs[2] + dtm * gs[3 + comp];
         acc = fmaf(S.r2[3 * leg[h] + comp], x[h] * drp[h], acc);  // valid slot: r2 of its leg
@@ -680,7 +843,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     for (int h = 0; h < 2; ++h) {
       const float Drl = Dr[h];
       const float Dinvl = __builtin_amdgcn_rcpf(Drl);
-      const f4v arz = S.arz[h][lxr];
+      const f4v arz = S.arz[wv][h][lxr];
       // E^-1 of the slot's rows from A~ = E A D (unit own-column entries)
       const f2v Einv = {valid[h] ? Drl * __builtin_amdgcn_rcpf(arz.x) : 1.0f,
                         (valid[h] && xy) ? Drl * __builtin_amdgcn_rcpf(arz.y) : 1.0f};
@@ -716,6 +879,14 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
 #pragma unroll
       for (int k = 0; k < 6; ++k) r[k] = wmax_nonneg(r[k]);
     }
+    if constexpr (W == 2) {  // block maxima (r only where the rho estimate needs them)
+      float v[12];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v[k] = o[k], v[6 + k] = want_r ? r[k] : 0.0f;
+      bcombine_max<W, 12>(S, v, wv);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) o[k] = v[k], r[k] = v[6 + k];
+    }
   };
 
   // warm start (x, z, y) before the first factorisation
@@ -739,7 +910,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         y[h].y = (valid[h] && xy) ? wy[rbase + 1] / e.y * cs : 0.0f;
         const float n1 = lane_next(x[h]), n2 = lane_next(n1);
         const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x[h]);
-        const f4v arz = S.arz[h][lxs];
+        const f4v arz = S.arz[wv][h][lxs];
         z[h] = (f2v){arz.x, arz.y} * x[h] + (f2v){arz.z, arz.w} * xz;
       }
     }
@@ -761,7 +932,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       auto w0_inv_row = [&](int h, float &i0, float &i1, float &i2) {
         float dinv_h = Dinv[h], csw = cs;
         asm volatile("" : "+v"(dinv_h), "+v"(csw));
-        const f4v arz = S.arz[h][lxf];
+        const f4v arz = S.arz[wv][h][lxf];
         const float rv0 = eq0[h] ? 1e3f * rho : rho, rv1 = rho;
         const float d_own = rv0 * arz.x * arz.x + rv1 * arz.y * arz.y;
         const float d_oz = rv0 * arz.x * arz.z + rv1 * arz.y * arz.w;
@@ -802,9 +973,9 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       for (int h = 0; h < 2; ++h) {
         float i0, i1, i2;
         w0_inv_row(h, i0, i1, i2);
-        S.w0i[0][h][lxf] = i0;
-        S.w0i[1][h][lxf] = i1;
-        S.w0i[2][h][lxf] = i2;
+        S.w0i[wv][0][h][lxf] = i0;
+        S.w0i[wv][1][h][lxf] = i1;
+        S.w0i[wv][2][h][lxf] = i2;
       }
       lsync();
       // U_j rows: wrench lane (jr, sr): U[sr][t] = sum_w Bb[sr][w] (W0^-1 Bb')[w][t]
@@ -814,9 +985,9 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
 #pragma unroll
         for (int g = 0; g < 4; ++g) {  // leg g of the step: 3 x 3 block
           const int v0 = base + 3 * g;
-          const f4v r0 = {S.w0i[0][hh][v0], S.w0i[1][hh][v0], S.w0i[2][hh][v0], 0.0f},
-                    r1 = {S.w0i[0][hh][v0 + 1], S.w0i[1][hh][v0 + 1], S.w0i[2][hh][v0 + 1], 0.0f},
-                    r2 = {S.w0i[0][hh][v0 + 2], S.w0i[1][hh][v0 + 2], S.w0i[2][hh][v0 + 2], 0.0f};
+          const f4v r0 = {S.w0i[wv][0][hh][v0], S.w0i[wv][1][hh][v0], S.w0i[wv][2][hh][v0], 0.0f},
+                    r1 = {S.w0i[wv][0][hh][v0 + 1], S.w0i[wv][1][hh][v0 + 1], S.w0i[wv][2][hh][v0 + 1], 0.0f},
+                    r2 = {S.w0i[wv][0][hh][v0 + 2], S.w0i[wv][1][hh][v0 + 2], S.w0i[wv][2][hh][v0 + 2], 0.0f};
           const float b0 = S.Bb[sr][3 * g], b1 = S.Bb[sr][3 * g + 1], b2 = S.Bb[sr][3 * g + 2];
           yv[3 * g + 0] = b0 * r0.x + b1 * r1.x + b2 * r2.x;
           yv[3 * g + 1] = b0 * r0.y + b1 * r1.y + b2 * r2.y;
@@ -827,7 +998,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
           float acc = 0.0f;
 #pragma unroll
           for (int w = 0; w < 12; ++w) acc = fmaf(yv[w], S.Bb[t][w], acc);
-          if (wvalid) S.U[jr][sr][t] = acc;
+          if (wvalid) S.U[wv][jr][sr][t] = acc;
         }
       }
       lsync();
@@ -839,7 +1010,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
 #pragma unroll
         for (int r = 0; r < 6; ++r)
 #pragma unroll
-          for (int c = 0; c < 6; ++c) Um[r][c] = wvalid ? S.U[jr][r][c] : (r == c ? 1.0f : 0.0f);
+          for (int c = 0; c < 6; ++c) Um[r][c] = wvalid ? S.U[wv][jr][r][c] : (r == c ? 1.0f : 0.0f);
         chol6(Um, L, Li);
 #pragma unroll
         for (int r = 0; r < 6; ++r) {
@@ -852,13 +1023,13 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
           Lcol[r] = lsr;
           if (lxf < 60) {
             if (r >= sr) {
-              S.Lt[jr][tri(sr) - sr + r] = lsr;   // column sr of L_j
-              S.Li[jr][tri(sr) - sr + r] = lisr;  // column sr of L_j^-1
+              S.Lt[jc][tri(sr) - sr + r] = lsr;   // column sr of L_j
+              S.Li[jc][tri(sr) - sr + r] = lisr;  // column sr of L_j^-1
             }
           }
         }
       }
-      lsync();
+      bsync<W>();
       // S = I + L' (cG) L, this lane's row: S[(jr,sr),(k,t)] = delta + c (K0 alpha.L_k[:,t] + K2 beta.L_k[:,t])
       float cS;  // c sS (the scaling below)
       {
@@ -885,46 +1056,59 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
             da = fmaf(al[s], Lcol[s], da);
             db = fmaf(be[s], Lcol[s], db);
           }
-          const f2v kk = S.k0k2[jr][jr];
+          const f2v kk = S.k0k2[jc][jc];
           const float dg = wvalid ? 1.0f + csf * fmaf(kk.x, da, kk.y * db) : 1.0f;
-          sS = 1.0f / wmax_nonneg(dg);
+          sS = 1.0f / bmax1<W>(S, wmax_nonneg(dg), wv);
         }
         cS = sgpr_f(csf * sS);
 #pragma unroll
-        for (int c = 0; c < 60; ++c) {
-          const int k = c / 6, t = c - 6 * (c / 6);
-          const float *lk = &S.Lt[k][tri(t) - t];  // column t of L_k (uniform): rows t..5
-          float da = 0.0f, db = 0.0f;
+        for (int wp = 0; wp < W; ++wp) {
 #pragma unroll
-          for (int s = t; s < 6; ++s) {
-            da = fmaf(al[s], lk[s], da);
-            db = fmaf(be[s], lk[s], db);
+          for (int c = 0; c < 60; ++c) {
+            const int k = c / 6, t = c - 6 * (c / 6);
+            const float *lk = &S.Lt[10 * wp + k][tri(t) - t];  // column t of L_k (uniform): rows t..5
+            float da = 0.0f, db = 0.0f;
+#pragma unroll
+            for (int s = t; s < 6; ++s) {
+              da = fmaf(al[s], lk[s], da);
+              db = fmaf(be[s], lk[s], db);
+            }
+            const f2v kk = S.k0k2[jc][10 * wp + k];
+            float v = cS * fmaf(kk.x, da, kk.y * db);
+            v = wvalid ? v : 0.0f;
+            T.k[60 * wp + c] = v + ((wp == wv && c == ln) ? sS : 0.0f);
+            // two waves: the entry is final here (otherwise the compiler sinks
+            // the row build into the Gauss-Jordan's first uses and keeps the L
+            // column reads of all 20 steps live across it: 276 spilled VGPRs)
+            if constexpr (W == 2) asm volatile("" : "+v"(T.k[60 * wp + c]));
           }
-          const f2v kk = S.k0k2[jr][k];
-          float v = cS * fmaf(kk.x, da, kk.y * db);
-          v = wvalid ? v : 0.0f;
-          T.k[c] = v + (c == ln ? sS : 0.0f);
         }
 #pragma unroll
-        for (int c = 60; c < 64; ++c) T.k[c] = 0.0f;
+        for (int c = 60 * W; c < 64 * W; ++c) T.k[c] = 0.0f;
       }
       // S^-1 in place
-      lit_invert(S, lxf, nw, T);
+      if constexpr (W == 1)
+        lit_invert(S, lxf, nw, T);
+      else
+        lit_invert2(S, wv, 6 * H, 6 * (N - H), T);
       // Z = S^-1 blockdiag(L_k^-1), this lane's row in place (L_k^-1 lower
       // triangular: column (k, t) from the columns (k, t' >= t))
 #pragma unroll
-      for (int k = 0; k < kLitN; ++k) {
-        float o[6];
+      for (int wp = 0; wp < W; ++wp) {
 #pragma unroll
-        for (int t = 0; t < 6; ++t) {
-          const float *li = &S.Li[k][tri(t) - t];  // column t of L_k^-1: rows t..5
-          float acc = 0.0f;
+        for (int k = 0; k < kLitN; ++k) {
+          float o[6];
 #pragma unroll
-          for (int tp = t; tp < 6; ++tp) acc = fmaf(T.k[6 * k + tp], li[tp], acc);
-          o[t] = acc;
+          for (int t = 0; t < 6; ++t) {
+            const float *li = &S.Li[10 * wp + k][tri(t) - t];  // column t of L_k^-1: rows t..5
+            float acc = 0.0f;
+#pragma unroll
+            for (int tp = t; tp < 6; ++tp) acc = fmaf(T.k[60 * wp + 6 * k + tp], li[tp], acc);
+            o[t] = acc;
+          }
+#pragma unroll
+          for (int t = 0; t < 6; ++t) T.k[60 * wp + 6 * k + t] = o[t];
         }
-#pragma unroll
-        for (int t = 0; t < 6; ++t) T.k[6 * k + t] = o[t];
       }
       // T = cG (L Z), four columns per pass, in place: the step's six rows give
       // M = L Z and Te M (= (Te L) Z), the horizon sums with K0 / K2 give
@@ -935,33 +1119,38 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         for (int c = 0; c < 6; ++c) {
           float tl = 0.0f;
 #pragma unroll
-          for (int r = c; r < 6; ++r) tl = fmaf(S.Te[sr][r], S.Lt[jr][tri(c) - c + r], tl);
+          for (int r = c; r < 6; ++r) tl = fmaf(S.Te[sr][r], S.Lt[jc][tri(c) - c + r], tl);
           tlrow[c] = tl;
         }
         const float qb = S.q2[6 + sr];
 #pragma unroll
-        for (int g = 0; g < 15; ++g) {
-          S.zc[lxf] = (f4v){T.k[4 * g], T.k[4 * g + 1], T.k[4 * g + 2], T.k[4 * g + 3]};
+        for (int g = 0; g < 15 * W; ++g) {
+          constexpr int zmask = W - 1;
+          const int zb = g & zmask;  // two waves: double-buffered by pass parity
+          S.zc[zb][wv][lxf] = (f4v){T.k[4 * g], T.k[4 * g + 1], T.k[4 * g + 2], T.k[4 * g + 3]};
           lsync();
           f4v m = (f4v)(0.0f), tm = (f4v)(0.0f);
 #pragma unroll
           for (int s2 = 0; s2 < 6; ++s2) {
-            const f4v zr = S.zc[6 * jr + s2];
-            const float lv = S.Lt[jr][tri(s2) - s2 + (sr > s2 ? sr : s2)];  // in bounds for every lane
+            const f4v zr = S.zc[zb][wv][6 * jr + s2];
+            const float lv = S.Lt[jc][tri(s2) - s2 + (sr > s2 ? sr : s2)];  // in bounds for every lane
             m = __builtin_elementwise_fma((f4v)(s2 <= sr ? lv : 0.0f), zr, m);
             tm = __builtin_elementwise_fma((f4v)(tlrow[s2]), zr, tm);
           }
           // L Z overwrites Z: the wave's LDS reads above complete in order first
           asm volatile("" ::: "memory");
-          S.zc[lxf] = m;
-          S.tc[lxf] = tm;
-          lsync();
+          S.zc[zb][wv][lxf] = m;
+          S.tc[zb][wv][lxf] = tm;
+          bsync<W>();
           f4v o0 = (f4v)(0.0f), o2 = (f4v)(0.0f);
 #pragma unroll
-          for (int k = 0; k < kLitN; ++k) {
-            const f2v kk = S.k0k2[jr][k];
-            o0 = __builtin_elementwise_fma((f4v)(kk.x), S.zc[6 * k + sr], o0);
-            o2 = __builtin_elementwise_fma((f4v)(kk.y), S.tc[6 * k + sr], o2);
+          for (int wp = 0; wp < W; ++wp) {
+#pragma unroll
+            for (int k = 0; k < kLitN; ++k) {
+              const f2v kk = S.k0k2[jc][10 * wp + k];
+              o0 = __builtin_elementwise_fma((f4v)(kk.x), S.zc[zb][wp][6 * k + sr], o0);
+              o2 = __builtin_elementwise_fma((f4v)(kk.y), S.tc[zb][wp][6 * k + sr], o2);
+            }
           }
           const f4v o = (f4v)(cS) * __builtin_elementwise_fma((f4v)(qb), o0, o2);
           T.k[4 * g + 0] = wvalid ? o.x : 0.0f;
@@ -969,7 +1158,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
           T.k[4 * g + 2] = wvalid ? o.z : 0.0f;
           T.k[4 * g + 3] = wvalid ? o.w : 0.0f;
         }
-        lsync();
+        bsync<W>();
       }
       // a = W0^-1 D^-1 b and x~ = D^-1 (a - W0^-1 t): this lane's row of W0^-1
       // as leg-triple shifts (D^-1 applied elementwise around the two dots)
@@ -1001,6 +1190,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         next = __builtin_amdgcn_readfirstlane(next);
         for (; iter < next; ++iter) {
           asm volatile("" ::: "memory");
+          const int par = W == 1 ? 0 : (iter & 1);  // two waves: broadcast rows double-buffered
           // rho vector (eq rows 1e3 rho) from the scalar rho each iteration: per-lane
           // selects instead of six loop-invariant registers
           float rr = rho_s, rvb = rvb_s;
@@ -1011,7 +1201,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
           float av[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const f4v arz = S.arz[h][lxi];
+            const f4v arz = S.arz[wv][h][lxi];
             const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
             const f2v rv = {rva[h][0], rva[h][1]};
             const f2v w = __builtin_elementwise_fma(rv, z[h], -y[h]);
@@ -1029,14 +1219,14 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
                   : "v"(tz), "v"(m2));
             }
             av[h] = tdot(Dinv[h] * rhs, W1[h]);  // W0^-1 D^-1 rhs
-            S.av[h][lxi] = av[h];
+            S.av[wv][h][lxi] = av[h];
           }
           lsync();
           // v = Vu a: wrench row (jr, sr) over its step's 12 variables
           float wr = 0.0f;
           {
             const int hh = jr >= 5 ? 1 : 0, base = 12 * (jr - 5 * hh);
-            const f4v *src = reinterpret_cast<const f4v *>(&S.av[hh][base]);
+            const f4v *src = reinterpret_cast<const f4v *>(&S.av[wv][hh][base]);
             const f4v u0 = src[0], u1 = src[1], u2 = src[2];
             const float uv[12] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w, u2.x, u2.y, u2.z, u2.w};
             const f4v *br = reinterpret_cast<const f4v *>(S.Bb[sr]);
@@ -1050,17 +1240,24 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
             }
             wr = w0 + w1;
           }
-          reinterpret_cast<float *>(&S.bc[0])[lxi] = wr;
-          lsync();
-          // s = T v (DPP broadcast matvec, 60 columns)
+          reinterpret_cast<float *>(&S.bc[par][wv][0])[lxi] = wr;
+          bsync<W>();
+          // s = T v (DPP broadcast matvec, 60 columns per half)
           float sv;
           {
-            const f4v r0 = S.bc[lxi & 15];
+            const f4v r0 = S.bc[par][0][lxi & 15];
             float acc0, acc1;
             QL_DPP_MATVEC60_2(acc0, acc1, r0, T.k, 0);
-            sv = acc0 + acc1;
+            if constexpr (W == 2) {
+              const f4v r1 = S.bc[par][1][lxi & 15];
+              float acc2, acc3;
+              QL_DPP_MATVEC60_2(acc2, acc3, r1, T.k, 60);
+              sv = (acc0 + acc1) + (acc2 + acc3);
+            } else {
+              sv = acc0 + acc1;
+            }
           }
-          S.wv[lxi] = sv;
+          S.wv[wv][lxi] = sv;
           lsync();
           // x~ = D^-1 a - D^-1 W0^-1 Vu' s, then update_x / update_z / update_y; the
           // variable's omega rows of B_d from LDS (a padding slot's are harmless:
@@ -1068,16 +1265,16 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
           const float bw0 = S.Bb[0][lxi % 12], bw1 = S.Bb[1][lxi % 12], bw2 = S.Bb[2][lxi % 12];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const float *gs = &S.wv[6 * step[h]];
+            const float *gs = &S.wv[wv][6 * stepl[h]];
             const f2v s01 = *reinterpret_cast<const f2v *>(gs), s23 = *reinterpret_cast<const f2v *>(gs + 2);
             f2v s45 = *reinterpret_cast<const f2v *>(gs + 4);
             asm volatile("" : "+v"(s45));  // loaded by every lane (no exec-masked load)
             const float sf = comp == 0 ? s23.y : (comp == 1 ? s45.x : s45.y);
             const float tv = fmaf(bw0, s01.x, fmaf(bw1, s01.y, fmaf(bw2, s23.x, dtm * sf)));
             const float xt = Dinv[h] * (av[h] - tdot(tv, W1[h]));  // D^-1 (a - W0^-1 t)
-            const f4v arz = S.arz[h][lxi];
+            const f4v arz = S.arz[wv][h][lxi];
             const f2v ra = {arz.x, arz.y}, rz = {arz.z, arz.w};
-            const float hi = S.zh[h][lxi];
+            const float hi = S.zh[wv][h][lxi];
             const f2v bnd = {xy ? 0.0f : zlo * hi, hi};
             const float n1 = lane_next(xt), n2 = lane_next(n1);
             const float xtz = comp == 0 ? n2 : n1;
@@ -1137,29 +1334,30 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
 
   // ---------------- 7. outputs: unscale, objective, leg slots (A1RobotControl.cpp:593-599)
   const int lane_o = fresh_lane();
+  const int tid_o = W == 1 ? lane_o : (int)threadIdx.x;
   float xu[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) xu[h] = valid[h] ? x[h] * Dr[h] : 0.0f;
   float ob = 0.0f;
 #pragma unroll
   for (int h = 0; h < 2; ++h) ob += valid[h] ? cinv * (0.5f * x[h] * px[h] + qv[h] * x[h]) : 0.0f;
-  const float objp = wsum(ob);
+  const float objp = bsum<W>(S, wsum(ob), wv);
   const bool bad = !isfinite(objp);
   if (bad) status = QLOCO_NAN;
   if (a.u) {
-    float *uo = a.u + b * 12 * N;
+    float *uo = a.u + b * 12 * N + 12 * so;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       if (valid[h]) uo[60 * h + lane_o] = bad ? NAN : xu[h];
   }
-  // u0: step-0 forces (variables 0..11 = slot 0, lanes 0..11); optional body frame R' u
+  // u0: step-0 forces (variables 0..11 = wave 0's slot 0, lanes 0..11); optional body frame R' u
   {
     const float n1 = lane_next(xu[0]), n2 = lane_next(n1);
     const float p1 = lane_prev(xu[0]), p2 = lane_prev(p1);
     const float f0 = comp == 0 ? xu[0] : (comp == 1 ? p1 : p2);
     const float f1 = comp == 0 ? n1 : (comp == 1 ? xu[0] : p1);
     const float f2 = comp == 0 ? n2 : (comp == 1 ? n1 : xu[0]);
-    if (lane_o < 12) {
+    if (tid_o < 12) {
       float o = xu[0];
       if (a.output_frame == 1) {  // R^T f with R = [[c,s,0],[-s,c,0],[0,0,1]], recomputed here
         const float yw = S.x0[2], cw = cosf(yw), sw = sinf(yw);
@@ -1170,7 +1368,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
   }
   if (prec) {  // the persistent record for the next call (layout QLOCO_SRBD_PERSIST_LEN)
     QL_LIT_LANE_INDICES(lxo);  // fresh indices: no address kept live from the warm start
-    for (int k = lane_o; k < NP + 4; k += 64) prec[k] = 0.0f;
+    for (int k = tid_o; k < NP + 4; k += 64 * W) prec[k] = 0.0f;
     __syncthreads();
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1189,8 +1387,8 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
         prec[64 * N + rbase + 1] = cinv * e.y * y[h].y;
       }
     }
-    for (int k = lane_o; k < 4 * N; k += 64) prec[96 * N + k] = S.ctf[k];
-    if (lane_o == 0) {
+    for (int k = tid_o; k < 4 * N; k += 64 * W) prec[96 * N + k] = S.ctf[k];
+    if (tid_o == 0) {
       prec[NP] = rho;
       prec[NP + 1] = 1.0f;
     }
@@ -1200,7 +1398,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
     const int nu = 12 * N, ncn = 20 * N;
     float *wx = a.warm + b * (nu + ncn);
     float *wy = wx + nu;
-    for (int k = lane_o; k < nu + ncn; k += 64) wx[k] = 0.0f;
+    for (int k = tid_o; k < nu + ncn; k += 64 * W) wx[k] = 0.0f;
     __syncthreads();
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1212,7 +1410,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
       if (xy) wy[rbase + 1] = cinv * e.y * y[h].y;
     }
   }
-  if (lane_o == 0) {
+  if (tid_o == 0) {
     if (a.status) a.status[b] = status;
     if (a.iters) a.iters[b] = iter;
     if (a.rho_updates) a.rho_updates[b] = rho_updates;
@@ -1223,19 +1421,37 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds &S, const
 template <bool WS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLitWpe)))
 void srbd_lit_kernel(const SrbdArgs a) {
-  __shared__ __attribute__((aligned(16))) LitLds S;
+  __shared__ __attribute__((aligned(16))) LitLds<1> S;
   const int64_t i = blockIdx.x;
   if (i >= a.batch) return;
-  srbd_lit_one<WS>(a, S, i);
+  srbd_lit_one<1, WS>(a, S, i);
+}
+
+template <bool WS>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(kLit2Wpe)))
+void srbd_lit2_kernel(const SrbdArgs a) {
+  __shared__ __attribute__((aligned(16))) LitLds<2> S;
+  const int64_t i = blockIdx.x;
+  if (i >= a.batch) return;
+  srbd_lit_one<2, WS>(a, S, i);
 }
 
 int srbd_lit_launch(const SrbdArgs &a, bool warm, hipStream_t stream) {
   const dim3 grid((unsigned)a.batch);
-  if (warm)
-    hipLaunchKernelGGL(srbd_lit_kernel<true>, grid, dim3(64), 0, stream, a);
-  else
-    hipLaunchKernelGGL(srbd_lit_kernel<false>, grid, dim3(64), 0, stream, a);
-  QLOCO_HIP_CHECK(hipGetLastError(), "srbd_lit_kernel launch");
+  if (a.N < 1 || a.N > kLitN2) return QLOCO_BAD_SIZE;
+  if (a.N <= kLitN) {
+    if (warm)
+      hipLaunchKernelGGL(srbd_lit_kernel<true>, grid, dim3(64), 0, stream, a);
+    else
+      hipLaunchKernelGGL(srbd_lit_kernel<false>, grid, dim3(64), 0, stream, a);
+    QLOCO_HIP_CHECK(hipGetLastError(), "srbd_lit_kernel launch");
+  } else {
+    if (warm)
+      hipLaunchKernelGGL(srbd_lit2_kernel<true>, grid, dim3(128), 0, stream, a);
+    else
+      hipLaunchKernelGGL(srbd_lit2_kernel<false>, grid, dim3(128), 0, stream, a);
+    QLOCO_HIP_CHECK(hipGetLastError(), "srbd_lit2_kernel launch");
+  }
   return QLOCO_OK;
 }
 

@@ -33,6 +33,26 @@ def gather_rows(total, world, mode=CONTIGUOUS):
     return rows
 
 
+def reorder(stage, total, world, mode=CONTIGUOUS, status_all=None, iters_all=None, stream=None):
+    """Gathered (world, P, width) shard rows -> u0 (total, 12) in global id
+    order on the device (qloco_mgpu_reorder: the reorder step of
+    qloco_mgpu_solve, for a caller that runs its own all-gather).  width 14
+    rows carry status / iterations as int32 bits in columns 12 / 13."""
+    import torch
+    width = int(stage.shape[-1])
+    P = -(-int(total) // int(world))
+    if (stage.dtype != torch.float32 or not stage.is_cuda or not stage.is_contiguous()
+            or stage.numel() != int(world) * P * width):
+        raise ValueError("stage: contiguous float32 device tensor of %d x %d x %d" % (world, P, width))
+    u0 = torch.empty((int(total), 12), dtype=torch.float32, device=stage.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(stage.device).cuda_stream
+    check(lib().qloco_mgpu_reorder(int(total), int(world), int(mode), width, ptr(stage), ptr(u0),
+                                   ptr(status_all), ptr(iters_all), C.c_void_p(stream)),
+          "qloco_mgpu_reorder")
+    return u0
+
+
 def unique_id():
     buf = (C.c_uint8 * ID_BYTES)()
     check(lib().qloco_mgpu_unique_id(buf), "qloco_mgpu_unique_id")
@@ -59,15 +79,20 @@ class MgpuSolver:
               "qloco_mgpu_info")
         self.first, self.count, self.stride, self.padded = f.value, c.value, s.value, p.value
         dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev  # the device the handle's communicator and buffers live on
         self.u0_all = torch.empty((self.total, 12), dtype=torch.float32, device=dev)
         self.status_all = torch.empty(self.total, dtype=torch.int32, device=dev)
         self.iters_all = torch.empty(self.total, dtype=torch.int32, device=dev)
 
     def solve(self, x0, x_ref, feet, contacts, stats=False, max_legs=0, warm=None, stream=None):
         import torch
+        from .srbd import check_inputs
         N = self.spec.horizon
         if x0.shape[0] != self.count:
             raise ValueError("this rank owns %d instances, got %d" % (self.count, x0.shape[0]))
+        # the checks BatchedConvexMpc.solve runs, on the handle's device: a CPU,
+        # float64 or non-contiguous tensor is refused before the C call
+        check_inputs(self.spec, x0, x_ref, feet, contacts, warm=warm, device=self.device)
         self.spec.feet_per_step = 1 if feet.shape[1] == 12 * N and N > 1 else 0
         self.spec.contacts_per_step = 1 if contacts.shape[1] == 4 * N and N > 1 else 0
         if stream is None:

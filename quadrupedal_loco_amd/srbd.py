@@ -79,6 +79,52 @@ def max_stance_legs(contacts, horizon, contacts_per_step=True):
     return per if contacts_per_step else per * horizon
 
 
+def warm_len(spec):
+    """Floats per instance of the warm-start buffer the spec's mode reads and
+    writes (include/qloco.h): 32N for warm_start = 1 (OSQP x | y), the
+    persistent record QLOCO_SRBD_PERSIST_LEN = 100N + 4 for warm_start = 2,
+    0 when off."""
+    N = int(spec.horizon)
+    return {0: 0, 1: 32 * N, 2: 100 * N + 4}.get(int(spec.warm_start), -1)
+
+
+def check_inputs(spec, x0, x_ref, feet, contacts, warm=None, device=None):
+    """Argument checks every SRBD entry point runs before a device pointer
+    reaches the C ABI (qloco_srbd_solve_ex, qloco_mgpu_solve): a CPU tensor,
+    a wrong dtype or a non-contiguous view is a ValueError here, not a GPU
+    memory fault.  Shapes: x0 (B, 13), x_ref (B, 13N), feet (B, 12) or
+    (B, 12N), contacts (B, 4) or (B, 4N); warm (B, warm_len(spec)) float32
+    when the spec's warm_start mode is on.  `device`: the device the tensors
+    must live on (default: x0's)."""
+    import torch
+    B = x0.shape[0]
+    N = int(spec.horizon)
+    dev = torch.device(device) if device is not None else x0.device
+    for name, t, dt in (("x0", x0, torch.float32), ("x_ref", x_ref, torch.float32),
+                        ("feet", feet, torch.float32), ("contacts", contacts, torch.uint8)):
+        if t.dtype != dt or not t.is_contiguous() or t.dim() != 2 or t.shape[0] != B:
+            raise ValueError("%s: need a contiguous 2-D %s tensor with batch %d" % (name, dt, B))
+        if not t.is_cuda:
+            raise ValueError("%s must be a device tensor (inputs resident in HBM)" % name)
+        if t.device != dev:
+            raise ValueError("%s is on %s, expected %s" % (name, t.device, dev))
+    if x0.shape[1] != 13 or x_ref.shape[1] != 13 * N:
+        raise ValueError("x0 (B,13) and x_ref (B,13N) expected")
+    if feet.shape[1] not in (12, 12 * N):
+        raise ValueError("feet (B,12) or (B,12N) expected")
+    if contacts.shape[1] not in (4, 4 * N):
+        raise ValueError("contacts (B,4) or (B,4N) expected")
+    wl = warm_len(spec)
+    if wl < 0:
+        raise ValueError("warm_start %d: 0, 1 or 2 expected" % spec.warm_start)
+    if wl:
+        if warm is None:
+            raise ValueError("warm_start %d needs a warm buffer (B, %d)" % (spec.warm_start, wl))
+        if (warm.dtype != torch.float32 or not warm.is_contiguous() or not warm.is_cuda
+                or warm.device != dev or warm.numel() != B * wl or warm.shape[0] != B):
+            raise ValueError("warm: need a contiguous float32 (%d, %d) tensor on %s" % (B, wl, dev))
+
+
 class BatchedConvexMpc:
     """Batched drop-in for ConvexMpc + OsqpEigen::Solver::solve.
 
@@ -115,14 +161,7 @@ class BatchedConvexMpc:
         import torch
         B = x0.shape[0]
         N = self.spec.horizon
-        for name, t, dt in (("x0", x0, torch.float32), ("x_ref", x_ref, torch.float32),
-                            ("feet", feet, torch.float32), ("contacts", contacts, torch.uint8)):
-            if t.dtype != dt or not t.is_contiguous() or t.shape[0] != B:
-                raise ValueError("%s: need contiguous %s with batch %d" % (name, dt, B))
-            if not t.is_cuda:
-                raise ValueError("%s must be a device tensor (inputs resident in HBM)" % name)
-        if x0.shape[1] != 13 or x_ref.shape[1] != 13 * N:
-            raise ValueError("x0 (B,13) and x_ref (B,13N) expected")
+        check_inputs(self.spec, x0, x_ref, feet, contacts, warm=warm)
         self.spec.feet_per_step = 1 if feet.shape[1] == 12 * N and N > 1 else 0
         self.spec.contacts_per_step = 1 if contacts.shape[1] == 4 * N and N > 1 else 0
         if self.spec.literal_full_qp:  # every (step, leg) pair is a variable

@@ -27,7 +27,14 @@ SPILL_BOUND = {
     "_ZN5qloco20srbd_admm_big_kernelILb0ELi120EEEvNS_8SrbdArgsE": 3,
     "_ZN5qloco15srbd_lit_kernelILb1EEEvNS_8SrbdArgsE": 28,                      # literal, persistent
     "_ZN5qloco15srbd_lit_kernelILb0EEEvNS_8SrbdArgsE": 24,                      # literal headline
+    "_ZN5qloco16srbd_lit2_kernelILb1EEEvNS_8SrbdArgsE": 2,                      # literal N 11..20, persistent
 }
+# two waves per SIMD, 128-thread workgroups (the literal QP at N = 11..20: a
+# 120-register row of S / T per lane)
+TWO_WAVE = [
+    "_ZN5qloco16srbd_lit2_kernelILb0EEEvNS_8SrbdArgsE",
+    "_ZN5qloco16srbd_lit2_kernelILb1EEEvNS_8SrbdArgsE",
+]
 # four waves per SIMD: 128 VGPRs and 16 one-wave workgroups' LDS per CU
 FOUR_WAVE = [
     "_ZN5qloco16srbd_admm_kernelILi1ELi4ELb0ELi10ELi16EEEvNS_8SrbdArgsE",
@@ -74,7 +81,7 @@ def kernels():
 
 def test_every_kernel_is_gfx950_and_listed(kernels):
     assert len(kernels) >= 30
-    for name in list(SPILL_BOUND) + FOUR_WAVE:
+    for name in list(SPILL_BOUND) + FOUR_WAVE + TWO_WAVE:
         assert name in kernels, name
 
 
@@ -95,3 +102,13 @@ def test_headline_kernels_fit_four_waves_per_simd(kernels):
         assert k[".group_segment_fixed_size"] <= 10240, (name, k[".group_segment_fixed_size"])
     # the reduced one-wave headline kernel has no scratch at all
     assert kernels[FOUR_WAVE[0]][".private_segment_fixed_size"] == 0
+
+
+def test_two_wave_literal_kernel_budget(kernels):
+    """The two-wave literal kernel: <= 256 registers (two waves
+    per SIMD), LDS for four workgroups per CU, the cold form spill-free."""
+    for name in TWO_WAVE:
+        k = kernels[name]
+        assert k[".vgpr_count"] + k[".agpr_count"] <= 256, (name, k[".vgpr_count"])
+        assert k[".group_segment_fixed_size"] <= 40960, (name, k[".group_segment_fixed_size"])
+    assert kernels[TWO_WAVE[0]][".vgpr_spill_count"] == 0

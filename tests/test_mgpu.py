@@ -133,3 +133,71 @@ def test_handle_world1_matches_single_gpu_solve(mode, gait, total):
         if stats:
             assert torch.equal(h.status_all, ref.status) and torch.equal(h.iters_all, ref.iters)
     h.close()
+
+
+def test_solve_refuses_bad_tensors_before_the_c_call():
+    """MgpuSolver.solve ran no input checks, so a CPU, float64 or
+    non-contiguous tensor reached qloco_mgpu_solve as a bad device pointer.
+    Both entry points now share srbd.check_inputs; every case below raises
+    ValueError on the host (no GPU needed, no C call made)."""
+    from quadrupedal_loco_amd import srbd
+    B, Nh = 4, 10
+    spec = srbd.default_spec(horizon=Nh)
+    x0 = torch.zeros((B, 13), dtype=torch.float32)
+    xr = torch.zeros((B, 13 * Nh), dtype=torch.float32)
+    ft = torch.zeros((B, 12), dtype=torch.float32)
+    ct = torch.ones((B, 4), dtype=torch.uint8)
+    h = mgpu.MgpuSolver.__new__(mgpu.MgpuSolver)  # no communicator: the checks come first
+    h.spec, h.count, h.device, h._h = spec, B, torch.device("cuda", 0), None
+    solver = srbd.BatchedConvexMpc(spec=spec)
+    bad = [
+        (x0, xr, ft, ct),                                      # CPU tensors
+        (x0.double(), xr, ft, ct),                             # float64
+        (x0, xr, torch.zeros((B, 24), dtype=torch.float32).t().contiguous().t()[:, :12], ct),
+        (x0, xr[:, :13 * Nh - 1], ft, ct),                     # x_ref width
+        (x0, xr, ft, ct.to(torch.int32)),                      # contacts dtype
+    ]
+    for args in bad:
+        with pytest.raises(ValueError):
+            h.solve(*args)
+        with pytest.raises(ValueError):
+            solver.solve(*args)
+    with pytest.raises(ValueError):  # this rank's instance count
+        h.solve(x0[:2], xr[:2], ft[:2], ct[:2])
+    spec2 = srbd.default_spec(horizon=Nh, warm_start=2)
+    assert srbd.warm_len(spec2) == srbd.persist_len(Nh) == 100 * Nh + 4
+    assert srbd.warm_len(srbd.default_spec(horizon=Nh, warm_start=1)) == 32 * Nh
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [mgpu.CONTIGUOUS, mgpu.INTERLEAVED])
+@pytest.mark.parametrize("total,world,width", [(13, 3, 12), (13, 3, 14), (4099, 8, 14), (16, 4, 12)])
+def test_device_reorder_matches_gather_rows(total, world, width, mode):
+    """the device reorder of qloco_mgpu_solve (mgpu_unpack_kernel,
+    padded shards, interleaved owners, the width-14 stats rows) had only run
+    at world 1, where it is skipped.  qloco_mgpu_reorder runs it on one GPU on
+    a synthetic gathered buffer for world > 1: every global id's row must land
+    where qloco_mgpu_gather_rows says, bit for bit, padding rows never read."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    dev = torch.device("cuda:0")
+    P = -(-total // world)
+    rng = np.random.default_rng(total * 31 + world)
+    stage = rng.standard_normal((world, P, width)).astype(np.float32)
+    rows = mgpu.gather_rows(total, world, mode)
+    if width == 14:  # status / iterations as int32 bits, distinct per global id
+        flat = stage.reshape(world * P, width)
+        flat[rows, 12] = np.arange(total, dtype=np.int32).view(np.float32)
+        flat[rows, 13] = (1000 + np.arange(total, dtype=np.int32)).view(np.float32)
+    pad = np.setdiff1d(np.arange(world * P), rows)
+    stage.reshape(world * P, width)[pad] = np.nan  # a padding row read would show up
+    d_stage = torch.from_numpy(stage).to(dev)
+    st = torch.full((total,), -1, dtype=torch.int32, device=dev) if width == 14 else None
+    it = torch.full((total,), -1, dtype=torch.int32, device=dev) if width == 14 else None
+    u0 = mgpu.reorder(d_stage, total, world, mode, status_all=st, iters_all=it)
+    torch.cuda.synchronize()
+    want = stage.reshape(world * P, width)[rows, :12]
+    assert np.array_equal(u0.cpu().numpy().view(np.int32), want.view(np.int32))
+    if width == 14:
+        assert np.array_equal(st.cpu().numpy(), np.arange(total))
+        assert np.array_equal(it.cpu().numpy(), 1000 + np.arange(total))

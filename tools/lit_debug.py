@@ -1,6 +1,6 @@
-"""Literal N <= 10 kernel: find the instances of a full batch that do not
-converge, re-solve them alone and against the fp64 restatement
-(development aid).  python tools/lit_debug.py [B] [gait]"""
+"""Literal wrench-space kernels: find the instances of a full batch that do
+not converge, re-solve them alone and against the fp64 restatement
+(development aid).  [N=16] python tools/lit_debug.py [B] [gait] [rho]"""
 import os
 import sys
 
@@ -16,7 +16,7 @@ from srbd_ref import Instance  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 gait = sys.argv[2] if len(sys.argv) > 2 else "trot"
-N = 10
+N = int(os.environ.get("N", 10))
 dev = torch.device("cuda:0")
 x0, xr, ft, ct = srbd.generate(20261015, N, B, gait)
 
@@ -31,7 +31,8 @@ def solve(idx, **kw):
 
 if len(sys.argv) > 3 and sys.argv[3] == "rho":
     sp = O.srbd_spec(N=N)
-    for b in (1454, 2647, 1):
+    bl = [int(x) for x in os.environ.get("INST", "1454,2647,1").split(",")]
+    for b in bl:
         inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
         for rho in (0.1, 1e-2, 1e-3, 3e-4, 1e-4, 1e-5):
             kw = dict(rho=rho, adaptive_rho=0, max_iter=600)
@@ -47,7 +48,8 @@ bad = np.nonzero(r["status"] != 0)[0]
 print("batch", B, gait, "status counts", np.unique(r["status"], return_counts=True), "iters mean",
       r["iters"].mean(), "max", r["iters"].max(), flush=True)
 sp = O.srbd_spec(N=N)
-for b in bad[:12]:
+print("bad", bad[:40].tolist(), flush=True)
+for b in bad[:6]:
     alone = solve(np.array([b]))
     inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
     xf, info = inst.admm_full()

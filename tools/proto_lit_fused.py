@@ -70,9 +70,9 @@ def solver(scaled):
 
 
 def main():
-    N = 10
+    N = int(os.environ.get("N", 10))
     ids = [int(a) for a in sys.argv[1:]] or [2647, 1]
-    x0, xr, ft, ct = srbd.generate(20261015, N, max(ids) + 1, "trot")
+    x0, xr, ft, ct = srbd.generate(20261015, N, max(ids) + 1, os.environ.get("GAIT", "trot"))
     sp = O.srbd_spec(N=N)
     base = P.WrenchSolve
     for b in ids:
