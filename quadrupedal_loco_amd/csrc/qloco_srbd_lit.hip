@@ -915,6 +915,15 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       }
     }
   }
+  // two waves: 1 / max diag G (G = K0 (x) Qb + K2 (x) Te depends on the
+  // instance only), the scaling of its Gauss-Jordan in every factorisation
+  float sGs = 1.0f;
+  if constexpr (W == 2) {
+    QL_LIT_LANE_INDICES(lxg);
+    const f2v kk = S.k0k2[jc][jc];
+    const float dg = wvalid ? fmaf(kk.y, S.Te[sr][sr], kk.x * S.q2[6 + sr]) : 0.0f;
+    sGs = sgpr_f(1.0f / bmax1<W>(S, wmax_nonneg(dg), wv));
+  }
   for (;;) {
     // ---------------- 6a. factorisation for the current rho
     {
@@ -979,6 +988,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       }
       lsync();
       // U_j rows: wrench lane (jr, sr): U[sr][t] = sum_w Bb[sr][w] (W0^-1 Bb')[w][t]
+      float Urow[6];  // two waves: this lane's row of U_jr stays in registers (padding: identity)
       {
         float yv[12];
         const int hh = jr >= 5 ? 1 : 0, base = 12 * (jr - 5 * hh);
@@ -998,9 +1008,14 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
           float acc = 0.0f;
 #pragma unroll
           for (int w = 0; w < 12; ++w) acc = fmaf(yv[w], S.Bb[t][w], acc);
-          if (wvalid) S.U[wv][jr][sr][t] = acc;
+          if constexpr (W == 1) {
+            if (wvalid) S.U[wv][jr][sr][t] = acc;
+          } else {
+            Urow[t] = wvalid ? acc : (t == sr ? 1.0f : 0.0f);
+          }
         }
       }
+      if constexpr (W == 1) {
       lsync();
       // per step: L_j (Cholesky of U_j), L_j^-1, rows of Te L_j -- every lane of
       // the step computes the factor, lane sr writes its row / column
@@ -1159,6 +1174,67 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
           T.k[4 * g + 3] = wvalid ? o.w : 0.0f;
         }
         bsync<W>();
+      }
+      } else {
+        // Two waves: T = (I + cG U)^-1 cG = (U + (cG)^-1)^-1.
+        // The S form above (pivot-free Gauss-Jordan on S = I + L'cGL, whose
+        // range grows with 1 / rho and the horizon) leaves a KKT backward
+        // error of 1e-3 .. 1e-2 at rho <= 3e-4 for N = 16 / 20, enough to stall
+        // ADMM on 1 in ~10^4 instances; M = U + (cG)^-1 keeps it at 1e-5 ..
+        // 5e-4 (float32 emulation, tools/lit_dump_t.py / DESIGN.md §3j).  G^-1
+        // by a Gauss-Jordan on the scaled G rows, then M = G^-1 / c + U (U
+        // block-diagonal: this lane's row of U_jr in its own step's six
+        // columns), scaled by 1 / max diag M and inverted in place.
+        {
+          const float qb = S.q2[6 + sr];
+          float ter[6];  // row sr of Te
+#pragma unroll
+          for (int t = 0; t < 6; ++t) ter[t] = S.Te[sr][t];
+#pragma unroll
+          for (int wp = 0; wp < W; ++wp) {
+#pragma unroll
+            for (int c = 0; c < 60; ++c) {
+              const int k = c / 6, t = c - 6 * (c / 6);
+              // G[(jc,sr),(k,t)] = K0 Qb_sr delta(sr, t) + K2 Te[sr][t]
+              const f2v kk = S.k0k2[jc][10 * wp + k];
+              const float g = fmaf(kk.y, ter[t], t == sr ? kk.x * qb : 0.0f);
+              const bool own = wp == wv && c == ln;
+              T.k[60 * wp + c] = sGs * (wvalid ? g : (own ? 1.0f : 0.0f));
+              asm volatile("" : "+v"(T.k[60 * wp + c]));  // final here (no sinking into the Gauss-Jordan)
+            }
+          }
+#pragma unroll
+          for (int c = 60 * W; c < 64 * W; ++c) T.k[c] = 0.0f;
+        }
+        lit_invert2(S, wv, 6 * H, 6 * (N - H), T);  // (sG G)^-1
+        float sM;
+        {
+          const float f1 = sgpr_f(sGs * cinv);  // G^-1 / c = (sG / c) (sG G)^-1
+          // 1 / max diag M, bounded without reading a lane's own (runtime-
+          // indexed) diagonal register: an SPD matrix's largest entry is on its
+          // diagonal, so max diag M <= max |G^-1| / c + max diag U (within 2x)
+          float gm = 0.0f, uii = 0.0f;
+#pragma unroll
+          for (int c = 0; c < 60 * W; ++c) gm = fmaxf(gm, fabsf(T.k[c]));
+#pragma unroll
+          for (int t = 0; t < 6; ++t) uii = t == sr ? Urow[t] : uii;
+          float mx[2] = {wmax_nonneg(wvalid ? gm : 0.0f), wmax_nonneg(wvalid ? uii : 0.0f)};
+          bcombine_max<W, 2>(S, mx, wv);
+          sM = sgpr_f(1.0f / fmaf(f1, mx[0], mx[1]));
+#pragma unroll
+          for (int wp = 0; wp < W; ++wp) {
+#pragma unroll
+            for (int c = 0; c < 60; ++c) {
+              const bool blk = wp == wv && c / 6 == jr;  // this row's own step block
+              const float ua = blk ? Urow[c % 6] : 0.0f;
+              T.k[60 * wp + c] = sM * fmaf(f1, T.k[60 * wp + c], ua);
+              asm volatile("" : "+v"(T.k[60 * wp + c]));
+            }
+          }
+        }
+        lit_invert2(S, wv, 6 * H, 6 * (N - H), T);  // (sM M)^-1
+#pragma unroll
+        for (int c = 0; c < 60 * W; ++c) T.k[c] *= sM;  // T = M^-1
       }
       // a = W0^-1 D^-1 b and x~ = D^-1 (a - W0^-1 t): this lane's row of W0^-1
       // as leg-triple shifts (D^-1 applied elementwise around the two dots)

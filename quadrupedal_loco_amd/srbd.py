@@ -51,6 +51,36 @@ def generate(seed, horizon, count, gait="trot", first=0, dt=0.0025, stride=1):
     return x0, xr, ft, ct
 
 
+def control_loop_sequence(seed, horizon, count, ticks, gait="trot", switch_every=None, dt=0.0025):
+    """Synthetic control-loop inputs for `count` controllers over `ticks` MPC
+    calls (the A1 GRF thread's 2.5 ms period, A1Params.h:10): the generated
+    instances drift as the robot would between ticks (position by v dt,
+    attitude by omega dt, the reference trajectory moving with them), and with
+    `switch_every` = K every controller flips its trot phase each K ticks (odd
+    controllers offset by K // 2).  Returns a list of (x0, x_ref, feet,
+    contacts) float32 / uint8 host arrays, one per tick."""
+    x0, xr, ft, ct = generate(seed, horizon, count, gait, dt=dt)
+    N, B = int(horizon), int(count)
+    seq = []
+    for t in range(ticks):
+        x = x0.astype(np.float64).copy()
+        r = xr.astype(np.float64).reshape(B, N, 13).copy()
+        dp = dt * t * x[:, 9:12]
+        da = 0.5 * dt * t * x[:, 6:9]
+        x[:, 3:6] += dp
+        x[:, 0:3] += da
+        r[:, :, 3:5] += dp[:, None, :2]
+        r[:, :, 2] += da[:, None, 2]
+        c = ct.copy()
+        if switch_every:
+            if (t // switch_every) % 2 == 1:
+                c[0::2] = 1 - c[0::2]
+            if ((t + switch_every // 2) // switch_every) % 2 == 1:
+                c[1::2] = 1 - c[1::2]
+        seq.append((x.astype(np.float32), r.reshape(B, 13 * N).astype(np.float32), ft.copy(), c))
+    return seq
+
+
 @dataclass
 class SrbdResult:
     u0: object              # (B, 12) first-step forces
