@@ -1605,7 +1605,13 @@ extern "C" int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, c
     }
   };
   const int top = srbd_class_of(legs, ws);
-  if (a.literal && a.N <= kLitN2 && !a.feet_per_step) {
+  // the wrench-space kernels build G^-1 from six N x N blocks (DESIGN.md
+  // §3j): that needs q_omega / q_v > 0 (G positive definite) and q_omega_x ==
+  // q_omega_y (the yaw rotation commutes with Q_omega); other weights take
+  // the generic literal kernels below
+  const bool lit_blocks = a.q2[6] == a.q2[7] && a.q2[6] > 0.0f && a.q2[8] > 0.0f &&
+                          a.q2[9] > 0.0f && a.q2[10] > 0.0f && a.q2[11] > 0.0f;
+  if (a.literal && a.N <= kLitN2 && !a.feet_per_step && lit_blocks) {
     // the literal QP at N <= 20 through the wrench space: one wave per
     // instance for N <= 10, two for 11..20 (qloco_srbd_lit.hip)
     const int rc = srbd_lit_launch(a, ws, st);

@@ -49,8 +49,8 @@ constexpr int kLit2Wpe = 2;  // two waves: 256 VGPRs (a 120-register row of S / 
 
 template <int W>
 struct LitLds {
-  // steps the per-step loops unroll over; the per-step tables (K0 / K2, L_j,
-  // L_j^-1, Ruiz column scales) are indexed by COLUMN-SPACE step 10 w' + kl
+  // steps the per-step loops unroll over; the per-step tables (K0 / K2, Ruiz
+  // column scales) are indexed by COLUMN-SPACE step 10 w' + kl
   // (wave w''s local step kl; two waves: the steps past a wave's N_w are
   // padding with zero K0 / K2 weights), so every table index in the unrolled
   // loops is a compile-time constant plus the wave's offset
@@ -77,17 +77,9 @@ struct LitLds {
       float Wc[12 * NT];
     };
     struct {                // factorisation
-      float Lt[NT][21];     // per step: columns of L_j, packed (column t: rows t..5 at tri(t))
-      float Li[NT][21];     // per step: columns of L_j^-1, packed the same way
-      union {
-        struct {
-          float w0i[W][3][2][64];   // per variable: its row of W0^-1 (x, y, z), until the U rows
-          float U[W][kLitN][6][6];  // per step: U_j (until its Cholesky)
-        };
-        struct {
-          f4v zc[W][W][64], tc[W][W][64];  // T passes: Z (then L Z, same wave, in order), Te L Z
-        };                                 // columns, [parity][wave]
-      };
+      float w0i[W][3][2][64];   // per variable its row of W0^-1 (x, y, z), read by the U rows
+      f4v gtab[NT][NT][2];      // G^-1 blocks: per (row step, column step) in
+                                // column-space order, (W0, W1, W2, V0), (V1, V2, -, -)
     };
   };
   float piv[W == 1 ? 0 : 2];       // two waves: the Gauss-Jordan pivot, [parity]
@@ -95,10 +87,6 @@ struct LitLds {
 };
 static_assert(sizeof(LitLds<1>) <= 10240, "literal kernel: four workgroups per SIMD need <= 160 KB / 16 of LDS");
 static_assert(sizeof(LitLds<2>) <= 40960, "two-wave literal kernel: four workgroups per CU need <= 40 KB");
-
-// Packed lower-triangular 6 x 6 columns: column t (rows t..5) starts at
-// tri(t); tri(t) - t + s addresses row s >= t.
-__device__ __forceinline__ constexpr int tri(int t) { return 6 * t - (t * (t - 1)) / 2; }
 
 // Wave-level helpers for the one-wave literal kernel
 __device__ __forceinline__ void lsync() {
@@ -296,42 +284,6 @@ __device__ __forceinline__ void lit_invert2(LitLds<2> &S, int wv, int nc0, int n
     lit2_pivot<0, 60 - decltype(kc)::value>(S, wv, nc0, K);
   });
   bsync<2>();
-}
-
-// 6 x 6 Cholesky L L' = A (lower, row-major a[r][c]) and L^-1, all in
-// registers (every lane of a step computes the same factor).
-__device__ __forceinline__ void chol6(const float (&a)[6][6], float (&L)[6][6], float (&Li)[6][6]) {
-#pragma unroll
-  for (int r = 0; r < 6; ++r)
-#pragma unroll
-    for (int c = 0; c < 6; ++c) L[r][c] = 0.0f, Li[r][c] = 0.0f;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    float d = a[i][i];
-#pragma unroll
-    for (int k = 0; k < i; ++k) d = fmaf(-L[i][k], L[i][k], d);
-    d = fmaxf(d, 1e-30f);
-    const float li = __builtin_amdgcn_rsqf(d);
-    L[i][i] = d * li;
-#pragma unroll
-    for (int r = i + 1; r < 6; ++r) {
-      float s = a[r][i];
-#pragma unroll
-      for (int k = 0; k < i; ++k) s = fmaf(-L[r][k], L[i][k], s);
-      L[r][i] = s * li;
-    }
-  }
-  // L^-1 (lower): forward substitution on the unit columns
-#pragma unroll
-  for (int c = 0; c < 6; ++c) {
-#pragma unroll
-    for (int r = c; r < 6; ++r) {
-      float s = r == c ? 1.0f : 0.0f;
-#pragma unroll
-      for (int k = c; k < r; ++k) s = fmaf(-L[r][k], Li[k][c], s);
-      Li[r][c] = s / L[r][r];
-    }
-  }
 }
 
 // Lane-derived indices re-derived from an opaque copy of the lane at the top
@@ -915,14 +867,75 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       }
     }
   }
-  // two waves: 1 / max diag G (G = K0 (x) Qb + K2 (x) Te depends on the
-  // instance only), the scaling of its Gauss-Jordan in every factorisation
-  float sGs = 1.0f;
-  if constexpr (W == 2) {
-    QL_LIT_LANE_INDICES(lxg);
-    const f2v kk = S.k0k2[jc][jc];
-    const float dg = wvalid ? fmaf(kk.y, S.Te[sr][sr], kk.x * S.q2[6 + sr]) : 0.0f;
-    sGs = sgpr_f(1.0f / bmax1<W>(S, wmax_nonneg(dg), wv));
+  // G^-1 in six N x N blocks.  G = K0 (x) Qb + K2 (x) Te
+  // (Qb = diag(q_omega, q_v), Te = dt^2 blockdiag(Rz' diag(q_theta) Rz,
+  // diag(q_p))) splits by wrench component: the v block is diagonal per axis,
+  // and with q_omega_x = q_omega_y (the host routes other weights elsewhere)
+  // the omega block is Rz' [K0 (x) Q_omega + K2 (x) dt^2 Q_theta] Rz.  So G^-1 is
+  // the inverses of A_a = alpha_a K0 + beta_a K2 (a = 3 omega axes, 3 v axes),
+  // recombined through Rz: one N x N Gauss-Jordan per (axis, row) lane in
+  // float64, once per solve, instead of a 6N x 6N one per factorisation.
+  float gmx;  // max diag G^-1 (block-uniform; an SPD matrix's largest entry)
+  {
+    double row[NS];
+    const int r = tid;
+    const bool live = r < 6 * N;
+    const int ax = live ? r / N : 0, ri = live ? r - N * (r / N) : 0;
+    {
+      const double dt2 = (double)dt * (double)dt;
+      const double al = ax < 3 ? (double)S.q2[6 + ax] : (double)S.q2[9 + ax - 3];
+      const double be = ax < 3 ? dt2 * (double)S.q2[ax] : dt2 * (double)S.q2[ax];  // q_theta / q_p: q2[0..5]
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        const int M = ri > k ? ri : k;
+        const double T0 = (double)(N - M), ia = (double)(M - ri), ib = (double)(M - k);
+        const double S1 = 0.5 * T0 * (T0 - 1.0), S2 = (T0 - 1.0) * T0 * (2.0 * T0 - 1.0) / 6.0;
+        const double K2 = S2 + (ia + ib) * S1 + ia * ib * T0;
+        row[k] = (live && k < N) ? fma(al, T0, be * K2) : (k == ri ? 1.0 : 0.0);
+      }
+    }
+    // in-place Gauss-Jordan, the pivot row through LDS (double-buffered in the
+    // table area, which is written only after the last pivot)
+    double *xch = reinterpret_cast<double *>(&S.gtab[0][0][0]);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      if (k >= N) continue;  // uniform; not a break (the loop must unroll: row[] stays in registers)
+      double *buf = xch + (k & 1) * (6 * NS);
+      if (live && ri == k) {
+#pragma unroll
+        for (int c = 0; c < NS; ++c) buf[ax * NS + c] = row[c];
+      }
+      bsync<W>();
+      const double *pr = buf + ax * NS;  // the pivot row, read as it is used (no second register row)
+      const double pinv = 1.0 / pr[k];
+      const double fk = row[k] * pinv;
+#pragma unroll
+      for (int c = 0; c < NS; ++c) {
+        if (c == k) continue;
+        const double pc = pr[c];
+        row[c] = ri == k ? pc * pinv : fma(-fk, pc, row[c]);
+      }
+      row[k] = ri == k ? pinv : -fk;
+    }
+    bsync<W>();
+    // the padding entries of the tables are zero
+    for (int idx = tid; idx < NT * NT * 2; idx += 64 * W) (&S.gtab[0][0][0])[idx] = (f4v)(0.0f);
+    bsync<W>();
+    float dmax = 0.0f;
+    if (live) {
+      const int csi = W == 1 ? ri : (ri < H ? ri : 10 + ri - H);
+      float *dst = reinterpret_cast<float *>(&S.gtab[csi][0][0]);
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        if (k < N) {
+          const int csk = W == 1 ? k : (k < H ? k : 10 + k - H);
+          dst[csk * 8 + ax] = (float)row[k];
+        }
+        dmax = k == ri ? (float)row[k] : dmax;
+      }
+    }
+    gmx = sgpr_f(bmax1<W>(S, wmax_nonneg(dmax), wv));
+    bsync<W>();
   }
   for (;;) {
     // ---------------- 6a. factorisation for the current rho
@@ -988,7 +1001,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       }
       lsync();
       // U_j rows: wrench lane (jr, sr): U[sr][t] = sum_w Bb[sr][w] (W0^-1 Bb')[w][t]
-      float Urow[6];  // two waves: this lane's row of U_jr stays in registers (padding: identity)
+      float Urow[6];  // this lane's row of U_jr, in registers (padding lanes: identity)
       {
         float yv[12];
         const int hh = jr >= 5 ? 1 : 0, base = 12 * (jr - 5 * hh);
@@ -1008,234 +1021,58 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
           float acc = 0.0f;
 #pragma unroll
           for (int w = 0; w < 12; ++w) acc = fmaf(yv[w], S.Bb[t][w], acc);
-          if constexpr (W == 1) {
-            if (wvalid) S.U[wv][jr][sr][t] = acc;
-          } else {
-            Urow[t] = wvalid ? acc : (t == sr ? 1.0f : 0.0f);
-          }
+          Urow[t] = wvalid ? acc : (t == sr ? 1.0f : 0.0f);
         }
       }
-      if constexpr (W == 1) {
-      lsync();
-      // per step: L_j (Cholesky of U_j), L_j^-1, rows of Te L_j -- every lane of
-      // the step computes the factor, lane sr writes its row / column
-      float Lcol[6];  // column sr of L_jr
+      // T = (I + cG U)^-1 cG = (U + (cG)^-1)^-1: this lane's
+      // row of M = G^-1 / c + U (G^-1 from the per-solve tables through the
+      // omega block's rotation; U block-diagonal: this lane's row of U_jr in
+      // its own step's six columns), scaled by 1 / (max diag G^-1 / c + max
+      // diag U) -- a bound within 2x of max diag M (SPD) -- and inverted in
+      // place.  (Round 4's S = I + L'cGL form left a KKT backward error of
+      // 1e-3 .. 1e-2 at rho <= 3e-4; M keeps it at 1e-5 .. 5e-4,
+      // tools/lit_numerics.py.)
+      float sM;
       {
-        float Um[6][6], L[6][6], Li[6][6];
+        float uii = 0.0f;
 #pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-          for (int c = 0; c < 6; ++c) Um[r][c] = wvalid ? S.U[wv][jr][r][c] : (r == c ? 1.0f : 0.0f);
-        chol6(Um, L, Li);
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-          float lsr = 0.0f, lisr = 0.0f;
-#pragma unroll
-          for (int c = 0; c < 6; ++c) {
-            lsr = (c == sr) ? L[r][c] : lsr;
-            lisr = (c == sr) ? Li[r][c] : lisr;
-          }
-          Lcol[r] = lsr;
-          if (lxf < 60) {
-            if (r >= sr) {
-              S.Lt[jc][tri(sr) - sr + r] = lsr;   // column sr of L_j
-              S.Li[jc][tri(sr) - sr + r] = lisr;  // column sr of L_j^-1
-            }
-          }
-        }
-      }
-      bsync<W>();
-      // S = I + L' (cG) L, this lane's row: S[(jr,sr),(k,t)] = delta + c (K0 alpha.L_k[:,t] + K2 beta.L_k[:,t])
-      float cS;  // c sS (the scaling below)
-      {
-        float al[6], be[6];
-#pragma unroll
-        for (int s = 0; s < 6; ++s) al[s] = S.q2[6 + s] * Lcol[s];
-#pragma unroll
-        for (int t = 0; t < 6; ++t) {
-          float acc = 0.0f;
-#pragma unroll
-          for (int s = 0; s < 6; ++s) acc = fmaf(Lcol[s], S.Te[s][t], acc);
-          be[t] = acc;
-        }
-        // S is built scaled by sS = 1 / max_r S[r][r]: the pivots of a Gauss-
-        // Jordan on an SPD matrix never exceed its largest diagonal entry, and
-        // the fused pivot-row update (A - A (1 - 1/p)) loses eps * p relative
-        // accuracy -- at small rho S reaches 1e4 and ADMM diverged (DESIGN.md
-        // §3i).  T = cG L S^-1 L^-1 = (c sS) G L (sS S)^-1 L^-1.
-        float sS;
-        {
-          float da = 0.0f, db = 0.0f;  // this lane's own column: L_jr[:, sr] = Lcol
-#pragma unroll
-          for (int s = 0; s < 6; ++s) {
-            da = fmaf(al[s], Lcol[s], da);
-            db = fmaf(be[s], Lcol[s], db);
-          }
-          const f2v kk = S.k0k2[jc][jc];
-          const float dg = wvalid ? 1.0f + csf * fmaf(kk.x, da, kk.y * db) : 1.0f;
-          sS = 1.0f / bmax1<W>(S, wmax_nonneg(dg), wv);
-        }
-        cS = sgpr_f(csf * sS);
+        for (int t = 0; t < 6; ++t) uii = t == sr ? Urow[t] : uii;
+        sM = sgpr_f(1.0f / fmaf(gmx, cinv, bmax1<W>(S, wmax_nonneg(wvalid ? uii : 0.0f), wv)));
+        // omega block coefficients Rz[a][sr] Rz[a][t], a, t in {0, 1}
+        // (Rz = [[c, s, 0], [-s, c, 0], [0, 0, 1]], A1RobotControl.cpp:506-508)
+        const float yw = S.x0[2], cw = cosf(yw), sw = sinf(yw);
+        const float r0 = sr == 0 ? cw : (sr == 1 ? sw : 0.0f), r1 = sr == 0 ? -sw : (sr == 1 ? cw : 0.0f);
+        const float c00 = r0 * cw, c01 = r0 * sw, c10 = -r1 * sw, c11 = r1 * cw;
+        const float m2 = sr == 2 ? 1.0f : 0.0f, m3 = sr == 3 ? 1.0f : 0.0f, m4 = sr == 4 ? 1.0f : 0.0f,
+                    m5 = sr == 5 ? 1.0f : 0.0f;
+        const float scale = sM * cinv;
 #pragma unroll
         for (int wp = 0; wp < W; ++wp) {
 #pragma unroll
-          for (int c = 0; c < 60; ++c) {
-            const int k = c / 6, t = c - 6 * (c / 6);
-            const float *lk = &S.Lt[10 * wp + k][tri(t) - t];  // column t of L_k (uniform): rows t..5
-            float da = 0.0f, db = 0.0f;
+          for (int k = 0; k < kLitN; ++k) {
+            const f4v e0 = S.gtab[jc][10 * wp + k][0], e1 = S.gtab[jc][10 * wp + k][1];
+            const float gv[6] = {fmaf(c00, e0.x, c10 * e0.y), fmaf(c01, e0.x, c11 * e0.y), m2 * e0.z,
+                                 m3 * e0.w, m4 * e1.x, m5 * e1.y};
+            const bool blk = wp == wv && k == jr;  // this row's own step block
 #pragma unroll
-            for (int s = t; s < 6; ++s) {
-              da = fmaf(al[s], lk[s], da);
-              db = fmaf(be[s], lk[s], db);
+            for (int t = 0; t < 6; ++t) {
+              const int c = 60 * wp + 6 * k + t;
+              const bool own = wp == wv && 6 * k + t == ln;
+              const float g = wvalid ? gv[t] : (own ? 1.0f : 0.0f);
+              T.k[c] = fmaf(scale, g, blk ? sM * Urow[t] : 0.0f);
+              asm volatile("" : "+v"(T.k[c]));  // final here (no sinking into the Gauss-Jordan)
             }
-            const f2v kk = S.k0k2[jc][10 * wp + k];
-            float v = cS * fmaf(kk.x, da, kk.y * db);
-            v = wvalid ? v : 0.0f;
-            T.k[60 * wp + c] = v + ((wp == wv && c == ln) ? sS : 0.0f);
-            // two waves: the entry is final here (otherwise the compiler sinks
-            // the row build into the Gauss-Jordan's first uses and keeps the L
-            // column reads of all 20 steps live across it: 276 spilled VGPRs)
-            if constexpr (W == 2) asm volatile("" : "+v"(T.k[60 * wp + c]));
           }
         }
 #pragma unroll
         for (int c = 60 * W; c < 64 * W; ++c) T.k[c] = 0.0f;
       }
-      // S^-1 in place
       if constexpr (W == 1)
-        lit_invert(S, lxf, nw, T);
+        lit_invert(S, lxf, nw, T);  // (sM M)^-1
       else
         lit_invert2(S, wv, 6 * H, 6 * (N - H), T);
-      // Z = S^-1 blockdiag(L_k^-1), this lane's row in place (L_k^-1 lower
-      // triangular: column (k, t) from the columns (k, t' >= t))
 #pragma unroll
-      for (int wp = 0; wp < W; ++wp) {
-#pragma unroll
-        for (int k = 0; k < kLitN; ++k) {
-          float o[6];
-#pragma unroll
-          for (int t = 0; t < 6; ++t) {
-            const float *li = &S.Li[10 * wp + k][tri(t) - t];  // column t of L_k^-1: rows t..5
-            float acc = 0.0f;
-#pragma unroll
-            for (int tp = t; tp < 6; ++tp) acc = fmaf(T.k[60 * wp + 6 * k + tp], li[tp], acc);
-            o[t] = acc;
-          }
-#pragma unroll
-          for (int t = 0; t < 6; ++t) T.k[60 * wp + 6 * k + t] = o[t];
-        }
-      }
-      // T = cG (L Z), four columns per pass, in place: the step's six rows give
-      // M = L Z and Te M (= (Te L) Z), the horizon sums with K0 / K2 give
-      // (cG M)[(j,s)] = c (Qb_s sum_k K0(j,k) M[(k,s)] + sum_k K2(j,k) (Te M)[(k,s)])
-      {
-        float tlrow[6];  // row sr of Te L_jr (from the packed columns); L's row is re-read per pass
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          float tl = 0.0f;
-#pragma unroll
-          for (int r = c; r < 6; ++r) tl = fmaf(S.Te[sr][r], S.Lt[jc][tri(c) - c + r], tl);
-          tlrow[c] = tl;
-        }
-        const float qb = S.q2[6 + sr];
-#pragma unroll
-        for (int g = 0; g < 15 * W; ++g) {
-          constexpr int zmask = W - 1;
-          const int zb = g & zmask;  // two waves: double-buffered by pass parity
-          S.zc[zb][wv][lxf] = (f4v){T.k[4 * g], T.k[4 * g + 1], T.k[4 * g + 2], T.k[4 * g + 3]};
-          lsync();
-          f4v m = (f4v)(0.0f), tm = (f4v)(0.0f);
-#pragma unroll
-          for (int s2 = 0; s2 < 6; ++s2) {
-            const f4v zr = S.zc[zb][wv][6 * jr + s2];
-            const float lv = S.Lt[jc][tri(s2) - s2 + (sr > s2 ? sr : s2)];  // in bounds for every lane
-            m = __builtin_elementwise_fma((f4v)(s2 <= sr ? lv : 0.0f), zr, m);
-            tm = __builtin_elementwise_fma((f4v)(tlrow[s2]), zr, tm);
-          }
-          // L Z overwrites Z: the wave's LDS reads above complete in order first
-          asm volatile("" ::: "memory");
-          S.zc[zb][wv][lxf] = m;
-          S.tc[zb][wv][lxf] = tm;
-          bsync<W>();
-          f4v o0 = (f4v)(0.0f), o2 = (f4v)(0.0f);
-#pragma unroll
-          for (int wp = 0; wp < W; ++wp) {
-#pragma unroll
-            for (int k = 0; k < kLitN; ++k) {
-              const f2v kk = S.k0k2[jc][10 * wp + k];
-              o0 = __builtin_elementwise_fma((f4v)(kk.x), S.zc[zb][wp][6 * k + sr], o0);
-              o2 = __builtin_elementwise_fma((f4v)(kk.y), S.tc[zb][wp][6 * k + sr], o2);
-            }
-          }
-          const f4v o = (f4v)(cS) * __builtin_elementwise_fma((f4v)(qb), o0, o2);
-          T.k[4 * g + 0] = wvalid ? o.x : 0.0f;
-          T.k[4 * g + 1] = wvalid ? o.y : 0.0f;
-          T.k[4 * g + 2] = wvalid ? o.z : 0.0f;
-          T.k[4 * g + 3] = wvalid ? o.w : 0.0f;
-        }
-        bsync<W>();
-      }
-      } else {
-        // Two waves: T = (I + cG U)^-1 cG = (U + (cG)^-1)^-1.
-        // The S form above (pivot-free Gauss-Jordan on S = I + L'cGL, whose
-        // range grows with 1 / rho and the horizon) leaves a KKT backward
-        // error of 1e-3 .. 1e-2 at rho <= 3e-4 for N = 16 / 20, enough to stall
-        // ADMM on 1 in ~10^4 instances; M = U + (cG)^-1 keeps it at 1e-5 ..
-        // 5e-4 (float32 emulation, tools/lit_dump_t.py / DESIGN.md §3j).  G^-1
-        // by a Gauss-Jordan on the scaled G rows, then M = G^-1 / c + U (U
-        // block-diagonal: this lane's row of U_jr in its own step's six
-        // columns), scaled by 1 / max diag M and inverted in place.
-        {
-          const float qb = S.q2[6 + sr];
-          float ter[6];  // row sr of Te
-#pragma unroll
-          for (int t = 0; t < 6; ++t) ter[t] = S.Te[sr][t];
-#pragma unroll
-          for (int wp = 0; wp < W; ++wp) {
-#pragma unroll
-            for (int c = 0; c < 60; ++c) {
-              const int k = c / 6, t = c - 6 * (c / 6);
-              // G[(jc,sr),(k,t)] = K0 Qb_sr delta(sr, t) + K2 Te[sr][t]
-              const f2v kk = S.k0k2[jc][10 * wp + k];
-              const float g = fmaf(kk.y, ter[t], t == sr ? kk.x * qb : 0.0f);
-              const bool own = wp == wv && c == ln;
-              T.k[60 * wp + c] = sGs * (wvalid ? g : (own ? 1.0f : 0.0f));
-              asm volatile("" : "+v"(T.k[60 * wp + c]));  // final here (no sinking into the Gauss-Jordan)
-            }
-          }
-#pragma unroll
-          for (int c = 60 * W; c < 64 * W; ++c) T.k[c] = 0.0f;
-        }
-        lit_invert2(S, wv, 6 * H, 6 * (N - H), T);  // (sG G)^-1
-        float sM;
-        {
-          const float f1 = sgpr_f(sGs * cinv);  // G^-1 / c = (sG / c) (sG G)^-1
-          // 1 / max diag M, bounded without reading a lane's own (runtime-
-          // indexed) diagonal register: an SPD matrix's largest entry is on its
-          // diagonal, so max diag M <= max |G^-1| / c + max diag U (within 2x)
-          float gm = 0.0f, uii = 0.0f;
-#pragma unroll
-          for (int c = 0; c < 60 * W; ++c) gm = fmaxf(gm, fabsf(T.k[c]));
-#pragma unroll
-          for (int t = 0; t < 6; ++t) uii = t == sr ? Urow[t] : uii;
-          float mx[2] = {wmax_nonneg(wvalid ? gm : 0.0f), wmax_nonneg(wvalid ? uii : 0.0f)};
-          bcombine_max<W, 2>(S, mx, wv);
-          sM = sgpr_f(1.0f / fmaf(f1, mx[0], mx[1]));
-#pragma unroll
-          for (int wp = 0; wp < W; ++wp) {
-#pragma unroll
-            for (int c = 0; c < 60; ++c) {
-              const bool blk = wp == wv && c / 6 == jr;  // this row's own step block
-              const float ua = blk ? Urow[c % 6] : 0.0f;
-              T.k[60 * wp + c] = sM * fmaf(f1, T.k[60 * wp + c], ua);
-              asm volatile("" : "+v"(T.k[60 * wp + c]));
-            }
-          }
-        }
-        lit_invert2(S, wv, 6 * H, 6 * (N - H), T);  // (sM M)^-1
-#pragma unroll
-        for (int c = 0; c < 60 * W; ++c) T.k[c] *= sM;  // T = M^-1
-      }
+      for (int c = 0; c < 60 * W; ++c) T.k[c] *= sM;  // T = M^-1
       // a = W0^-1 D^-1 b and x~ = D^-1 (a - W0^-1 t): this lane's row of W0^-1
       // as leg-triple shifts (D^-1 applied elementwise around the two dots)
 #pragma unroll

@@ -798,6 +798,35 @@ def test_srbd_literal_full_size_sampled(N, B, gait, samples):
     u0b.check()
 
 
+@pytest.mark.parametrize("N,B,gait,qpatch", [(10, 16, "trot", {7: 0.2}), (16, 12, "trot", {6: 0.5})])
+def test_srbd_literal_weights_outside_the_block_tables(N, B, gait, qpatch):
+    """The wrench-space kernels' G^-1 tables need q_omega_x == q_omega_y and
+    q_omega, q_v > 0; other weights (here an anisotropic
+    omega weight at N = 10 and N = 16) take the generic literal kernels
+    (two-wave column bucket / wide kernel).  Same bounds against the
+    restatement of the same QP as test_srbd_literal_matches_full_restatement
+    (status, iterations within one check, objective, swing forces, u0)."""
+    q = list(O.Q_W)
+    for k, v in qpatch.items():
+        q[k] = v
+    (x0, xr, ft, ct), r = _solve(N, B, gait, literal_full_qp=1, q_weights=q)
+    sp = O.srbd_spec(N=N, q_w=q)
+    u0b = U0Bound()
+    for b in range(B):
+        inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
+        xf, info = inst.admm_full()
+        assert r["status"][b] == 0 and info.status == 0, (b, r["status"][b], info.status)
+        assert abs(int(r["iters"][b]) - info.iters) <= 25, (b, r["iters"][b], info.iters)
+        u = r["u"][b].astype(np.float64)
+        du0, dF, dM, dX = _traj_metrics(u, xf, x0[b], xr[b], ft[b], ct[b], N)
+        u0b.add(du0, int(r["iters"][b]) == info.iters, b)
+        sc = max(1.0, abs(inst.obj(xf)))
+        assert abs(inst.obj(u) - inst.obj(xf)) <= 5e-3 * sc, (b, inst.obj(u), inst.obj(xf))
+        swing = np.repeat(ct[b] == 0, 3)
+        assert np.all(np.abs(u[swing]) <= 0.25), (b, np.abs(u[swing]).max())
+    u0b.check()
+
+
 def test_srbd_literal_edge_cases_and_modes():
     """Literal mode corner cases: an all-swing instance (every fz row an
     equality [0, 0]: the optimum is u = 0), an all-stance one and a
