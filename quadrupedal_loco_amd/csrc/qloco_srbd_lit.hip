@@ -37,6 +37,7 @@
 // so a lane's row of S / T is 60 W registers and the Gauss-Jordan and the
 // matvec are W of the one-wave kernel's 60-column DPP forms.
 #include <math.h>
+#include <stddef.h>
 
 #include <type_traits>
 
@@ -69,7 +70,19 @@ struct LitLds {
   f4v arz[W][2][64];        // per slot: scaled A entries (ra0, ra1, rz0, rz1)
   float zh[W][2][64];       // per slot: row 0's scaled upper bound (x / y rows: inf); the lower
                             // bound is 0 (x / y) or zh fz_min / fz_max (z rows)
-  union {                   // phase-local storage (LDS bounds the one-wave occupancy: <= 10 KB)
+  float dr[W][2][64];       // per slot: the Ruiz column scale D (read where needed: not a
+                            // register live across the ADMM loop)
+  float qvl[W][2][64];      // per slot: the scaled gradient q~ (read where needed)
+  // block-uniform solver state, one copy per wave (both waves take identical
+  // decisions): read into SGPRs where a phase needs it, so no register carries
+  // it across the ADMM iterations
+  struct {
+    float rho, cs, cinv, qn0, qn1, alpha, oma, sigma, dtm;
+    int iter, status, rho_updates, ctm, interval;
+  } sc[W];
+  union alignas(16) {       // phase-local storage (LDS bounds the one-wave occupancy: <= 10 KB;
+                            // 16-byte aligned: dcol is read as f4v, a misaligned ds_read_b128
+                            // cost the one-wave kernel 46 us per launch)
     struct {                // gradient + Ruiz
       f2v beps[12][12];     // (beta, eps)[w][w']: the P entries' per-column coefficients
       float dcol[12 * NT];  // Ruiz column scales D (read as same-address broadcasts)
@@ -78,8 +91,8 @@ struct LitLds {
     };
     struct {                // factorisation
       float w0i[W][3][2][64];   // per variable its row of W0^-1 (x, y, z), read by the U rows
-      f4v gtab[NT][NT][2];      // G^-1 blocks: per (row step, column step) in
-                                // column-space order, (W0, W1, W2, V0), (V1, V2, -, -)
+      f2v gtab[NT][NT][3];      // G^-1 blocks: per (row step, column step) in
+                                // column-space order, (W0, W1), (W2, V0), (V1, V2)
     };
   };
   float piv[W == 1 ? 0 : 2];       // two waves: the Gauss-Jordan pivot, [parity]
@@ -87,6 +100,8 @@ struct LitLds {
 };
 static_assert(sizeof(LitLds<1>) <= 10240, "literal kernel: four workgroups per SIMD need <= 160 KB / 16 of LDS");
 static_assert(sizeof(LitLds<2>) <= 40960, "two-wave literal kernel: four workgroups per CU need <= 40 KB");
+static_assert(offsetof(LitLds<1>, dcol) % 16 == 0 && offsetof(LitLds<2>, dcol) % 16 == 0,
+              "dcol is read as f4v (ds_read_b128 needs 16-byte alignment)");
 
 // Wave-level helpers for the one-wave literal kernel
 __device__ __forceinline__ void lsync() {
@@ -473,7 +488,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
     }
   }
   bsync<W>();
-  float qv[2], qsv[2], q_raw[2];
+  float qv[2], qsv[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     float g = 0.0f;
@@ -484,7 +499,6 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       g += dtm * w[9 + comp] + dt2m * w[3 + comp];
     }
     qv[h] = g;
-    q_raw[h] = g;
     qsv[h] = g;
   }
   // from here on a variable's B_d column is all the iterations need of lo/hi:
@@ -500,6 +514,11 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       if (valid[h]) qsv[h] = prec[84 * N + 12 * step[h] + 3 * leg[h] + comp];
+  }
+  if (prec) {  // the record's q for the next call, written now (each variable's own entry, just read)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (valid[h]) prec[84 * N + 12 * step[h] + 3 * leg[h] + comp] = qv[h];
   }
 
   // ---------------- 4. constraint rows owned by each slot (ConvexMpc.cpp:47-59, :227-249)
@@ -668,7 +687,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
   // block-uniform scalars live in SGPRs (a VGPR copy would be kept, and
   // spilled, across the whole ADMM loop)
   cs = sgpr_f(cs);
-  const float cinv = sgpr_f(1.0f / cs);
+  const float cinv0 = sgpr_f(1.0f / cs);
   bool eq0[2];
   float qn[2] = {0.0f, 0.0f};
 #pragma unroll
@@ -676,6 +695,8 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
     const float lh0 = rl0[h] * rE0[h], uh0 = ru0[h] * rE0[h];
     eq0[h] = valid[h] && !xy && (uh0 - lh0 < 1e-4f);  // OSQP set_rho_vec: RHO_TOL
     S.zh[wv][h][lane] = uh0;
+    S.dr[wv][h][lane] = Dr[h];
+    S.qvl[wv][h][lane] = qv[h];
     S.arz[wv][h][lane] = (f4v){ra0[h], ra1[h], rz0[h], rz1[h]};
     qn[0] = fmaxf(qn[0], valid[h] ? fabsf(qv[h] / Dr[h]) : 0.0f);
     qn[1] = fmaxf(qn[1], valid[h] ? fabsf(qv[h]) : 0.0f);
@@ -683,13 +704,18 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
   qn[0] = wmax_nonneg(qn[0]);
   qn[1] = wmax_nonneg(qn[1]);
   bcombine_max<W, 2>(S, qn, wv);
+  S.sc[wv].cs = cs;  // every lane the same value
+  S.sc[wv].cinv = cinv0;
+  S.sc[wv].qn0 = qn[0];
+  S.sc[wv].qn1 = qn[1];
   lsync();
 
   // row scaling E of a slot's two rows, from A~ = E A D (each row's entry in
   // its own variable's column is 1 before scaling)
   auto row_e = [&](int h) -> f2v {
-    const f4v arz = S.arz[wv][h][fresh_lane()];
-    const float d = Dr[h];
+    const int fl = fresh_lane();
+    const f4v arz = S.arz[wv][h][fl];
+    const float d = S.dr[wv][h][fl];
     return (f2v){valid[h] ? arz.x / d : 1.0f, (valid[h] && xy) ? arz.y / d : 1.0f};
   };
 
@@ -702,29 +728,36 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
   // the factorisation's bound); padding wrench lanes get zeros
   // through their K0 / K2 weights and masks
   // this lane's variables' wrench columns (omega rows = lo.xyz, v row = dtm at comp)
-  float rho = sgpr_f(fminf(fmaxf(p_same ? prec[NP] : a.rho, 1e-6f), 1e6f));
+  S.sc[wv].rho = sgpr_f(fminf(fmaxf(p_same ? prec[NP] : a.rho, 1e-6f), 1e6f));
 
   // ---------------- 6. ADMM (osqp_solve) with its (re)factorisations
   float x[2] = {0.0f, 0.0f};
   f2v z[2] = {(f2v)(0.0f), (f2v)(0.0f)}, y[2] = {(f2v)(0.0f), (f2v)(0.0f)};
-  const float alpha = a.alpha, oma = 1.0f - a.alpha, sigma = a.sigma;
-  const int ctm = a.check_termination;
-  const int interval = (a.adaptive_rho && a.rho_interval == 0) ? (ctm ? 4 * ctm : 100)
-                                                               : (a.adaptive_rho ? a.rho_interval : 0);
-  int status = QLOCO_MAX_ITER, iter = 0, rho_updates = 0;
-  float px[2] = {0.0f, 0.0f};
+  {
+    S.sc[wv].alpha = a.alpha;
+    S.sc[wv].oma = 1.0f - a.alpha;
+    S.sc[wv].sigma = a.sigma;
+    S.sc[wv].dtm = dtm;
+    const int ctm = a.check_termination;
+    S.sc[wv].ctm = ctm;
+    S.sc[wv].interval = (a.adaptive_rho && a.rho_interval == 0) ? (ctm ? 4 * ctm : 100)
+                                                                : (a.adaptive_rho ? a.rho_interval : 0);
+    S.sc[wv].iter = 0;
+    S.sc[wv].status = QLOCO_MAX_ITER;
+    S.sc[wv].rho_updates = 0;
+  }
+  lsync();
+  auto uf = [&](const float &v) { return sgpr_f(v); };  // an LDS scalar into an SGPR
+  auto ui = [&](const int &v) { return __builtin_amdgcn_readfirstlane(v); };
   Row<W> T;        // T = (I + cG U)^-1 cG, this lane's wrench row (column space)
   Shift5 W1[2];  // per slot: this lane's row of W0^-1 as leg-triple shifts
-  float Dinv[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) Dinv[h] = valid[h] ? 1.0f / Dr[h] : 0.0f;
 
   // P~ x (scaled) per slot: c D (Vu' G Vu + R) D x through the wrench rows
   auto p_times_x = [&](float (&out)[2]) {
     if constexpr (W == 2) bsync<W>();  // the other wave is done with the iteration's broadcast rows
     QL_LIT_LANE_INDICES(lxp);
-    float drp[2] = {Dr[0], Dr[1]};  // opaque: cs D is not hoisted into the loop-live set
-    asm volatile("" : "+v"(drp[0]), "+v"(drp[1]));
+    const float drp[2] = {S.dr[wv][0][lxp], S.dr[wv][1][lxp]};
+    const float csl = uf(S.sc[wv].cs), dtm = uf(S.sc[wv].dtm);
 #pragma unroll
     for (int h = 0; h < 2; ++h) S.av[wv][h][lxp] = valid[h] ? x[h] * drp[h] : 0.0f;
     lsync();
@@ -781,19 +814,20 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
         acc = S.Bb[0][wc] * gs[0] + S.Bb[1][wc] * gs[1] + S.Bb[2][wc] * gs[2] + dtm * gs[3 + comp];
         acc = fmaf(S.r2[3 * leg[h] + comp], x[h] * drp[h], acc);  // valid slot: r2 of its leg
       }
-      out[h] = cs * drp[h] * acc;
+      out[h] = csl * drp[h] * acc;
     }
     lsync();
   };
 
   auto residuals = [&](float (&o)[6], float (&r)[6], bool want_r) {
+    float px[2];
     p_times_x(px);
     QL_LIT_LANE_INDICES(lxr);
 #pragma unroll
     for (int k = 0; k < 6; ++k) o[k] = r[k] = 0.0f;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const float Drl = Dr[h];
+      const float Drl = S.dr[wv][h][lxr];
       const float Dinvl = __builtin_amdgcn_rcpf(Drl);
       const f4v arz = S.arz[wv][h][lxr];
       // E^-1 of the slot's rows from A~ = E A D (unit own-column entries)
@@ -806,7 +840,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       const float ay_z = az.x + az.y;
       const float p1 = lane_prev(ay_z), p2 = lane_prev(p1);
       const float aty = valid[h] ? ((ay.x + ay.y) + (comp == 2 ? (p1 + p2) : 0.0f)) : 0.0f;
-      const float rd = valid[h] ? (qv[h] + px[h] + aty) : 0.0f;
+      const float rd = valid[h] ? (S.qvl[wv][h][lxr] + px[h] + aty) : 0.0f;
       const f2v ax = ra * x[h] + rz * xz;
       const f2v rp = ax - z[h];
       const f2v erp = Einv * rp, ez = Einv * z[h], eax = Einv * ax;
@@ -856,10 +890,11 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       } else if (a.warm_start == 1) {
         const float *wx = a.warm + b * (32 * N);
         const float *wy = wx + 12 * N;
-        x[h] = valid[h] ? wx[vidx] / Dr[h] : 0.0f;
+        x[h] = valid[h] ? wx[vidx] / S.dr[wv][h][lxs] : 0.0f;
         const f2v e = row_e(h);
-        y[h].x = valid[h] ? wy[rbase] / e.x * cs : 0.0f;
-        y[h].y = (valid[h] && xy) ? wy[rbase + 1] / e.y * cs : 0.0f;
+        const float csl = uf(S.sc[wv].cs);
+        y[h].x = valid[h] ? wy[rbase] / e.x * csl : 0.0f;
+        y[h].y = (valid[h] && xy) ? wy[rbase + 1] / e.y * csl : 0.0f;
         const float n1 = lane_next(x[h]), n2 = lane_next(n1);
         const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x[h]);
         const f4v arz = S.arz[wv][h][lxs];
@@ -897,6 +932,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
     // in-place Gauss-Jordan, the pivot row through LDS (double-buffered in the
     // table area, which is written only after the last pivot)
     double *xch = reinterpret_cast<double *>(&S.gtab[0][0][0]);
+    static_assert(sizeof(S.gtab) >= 2 * 6 * NS * sizeof(double), "pivot-row exchange fits the table area");
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
       if (k >= N) continue;  // uniform; not a break (the loop must unroll: row[] stays in registers)
@@ -919,7 +955,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
     }
     bsync<W>();
     // the padding entries of the tables are zero
-    for (int idx = tid; idx < NT * NT * 2; idx += 64 * W) (&S.gtab[0][0][0])[idx] = (f4v)(0.0f);
+    for (int idx = tid; idx < NT * NT * 3; idx += 64 * W) (&S.gtab[0][0][0])[idx] = (f2v)(0.0f);
     bsync<W>();
     float dmax = 0.0f;
     if (live) {
@@ -929,7 +965,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       for (int k = 0; k < NS; ++k) {
         if (k < N) {
           const int csk = W == 1 ? k : (k < H ? k : 10 + k - H);
-          dst[csk * 8 + ax] = (float)row[k];
+          dst[csk * 6 + ax] = (float)row[k];
         }
         dmax = k == ri ? (float)row[k] : dmax;
       }
@@ -943,8 +979,8 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       // opaque per factorisation: nothing derived from these is hoisted out of
       // the refactor loop (it would stay live through the ADMM iterations)
       int ln = fresh_lane();
-      float csf = cs;
-      asm volatile("" : "+v"(ln), "+v"(csf));
+      asm volatile("" : "+v"(ln));
+      const float rho = uf(S.sc[wv].rho), cinv = uf(S.sc[wv].cinv), sigma = uf(S.sc[wv].sigma);
       QL_LIT_LANE_INDICES(lxf);
       // this lane's row of W0^-1 for slot h (W0 = D^-1 (sigma I + A~' rho A~) D^-1 +
       // c R, 3 x 3 per leg): written for the U rows, recomputed for the
@@ -952,7 +988,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       // (D^-1 and c re-laundered per call: the first call's copies do not stay
       // live across S^-1 for the second)
       auto w0_inv_row = [&](int h, float &i0, float &i1, float &i2) {
-        float dinv_h = Dinv[h], csw = cs;
+        float dinv_h = valid[h] ? 1.0f / S.dr[wv][h][lxf] : 0.0f, csw = uf(S.sc[wv].cs);
         asm volatile("" : "+v"(dinv_h), "+v"(csw));
         const f4v arz = S.arz[wv][h][lxf];
         const float rv0 = eq0[h] ? 1e3f * rho : rho, rv1 = rho;
@@ -1050,9 +1086,10 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
         for (int wp = 0; wp < W; ++wp) {
 #pragma unroll
           for (int k = 0; k < kLitN; ++k) {
-            const f4v e0 = S.gtab[jc][10 * wp + k][0], e1 = S.gtab[jc][10 * wp + k][1];
-            const float gv[6] = {fmaf(c00, e0.x, c10 * e0.y), fmaf(c01, e0.x, c11 * e0.y), m2 * e0.z,
-                                 m3 * e0.w, m4 * e1.x, m5 * e1.y};
+            const f2v e0 = S.gtab[jc][10 * wp + k][0], e1 = S.gtab[jc][10 * wp + k][1],
+                      e2 = S.gtab[jc][10 * wp + k][2];
+            const float gv[6] = {fmaf(c00, e0.x, c10 * e0.y), fmaf(c01, e0.x, c11 * e0.y), m2 * e1.x,
+                                 m3 * e1.y, m4 * e2.x, m5 * e2.y};
             const bool blk = wp == wv && k == jr;  // this row's own step block
 #pragma unroll
             for (int t = 0; t < 6; ++t) {
@@ -1086,18 +1123,27 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
     bool refactor = false;
 
     for (;;) {
+      int iter = ui(S.sc[wv].iter);
+      const int ctm = ui(S.sc[wv].ctm), interval = ui(S.sc[wv].interval);
       if (iter < a.max_iter) {
         int next = a.max_iter;
-        // opaque divisors: the reciprocal constants of the two divisions are
-        // recomputed per block instead of held in VGPRs for the whole kernel
-        int ctl = ctm, itl = interval;
-        asm volatile("" : "+s"(ctl), "+s"(itl));
-        if (ctl) next = min(next, (iter / ctl + 1) * ctl);
-        if (itl) next = min(next, (iter / itl + 1) * itl);
-        const float rho_s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rho)));
-        const float rvb_s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, 1.0f / rho)));
+        if (ctm) next = min(next, (iter / ctm + 1) * ctm);
+        if (interval) next = min(next, (iter / interval + 1) * interval);
+        const float rho = uf(S.sc[wv].rho);
+        const float rho_s = rho;
+        const float rvb_s = sgpr_f(1.0f / rho);
         const float zlo = a.fz_max > 0.0f ? a.fz_min / a.fz_max : 0.0f;  // z rows: lower = zlo upper
         QL_LIT_LANE_INDICES(lxi);
+        // loop operands read here, per segment of iterations: none is a register
+        // across the residual checks and factorisations
+        const float alpha = uf(S.sc[wv].alpha), oma = uf(S.sc[wv].oma), sigma = uf(S.sc[wv].sigma),
+                    dtm = uf(S.sc[wv].dtm);
+        float qvr[2], Dinv[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          qvr[h] = S.qvl[wv][h][lxi];
+          Dinv[h] = valid[h] ? 1.0f / S.dr[wv][h][lxi] : 0.0f;
+        }
         // wave-uniform trip count (a scalar loop, not an exec-masked one)
         iter = __builtin_amdgcn_readfirstlane(iter);
         next = __builtin_amdgcn_readfirstlane(next);
@@ -1120,7 +1166,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
             const f2v w = __builtin_elementwise_fma(rv, z[h], -y[h]);
             const f2v aw = ra * w, zw = rz * w;
             const float tz = zw.x + zw.y;
-            float rhs = fmaf(sigma, x[h], (aw.x + aw.y) - qv[h]);
+            float rhs = fmaf(sigma, x[h], (aw.x + aw.y) - qvr[h]);
             {
               const float m2 = comp == 2 ? 1.0f : 0.0f;
               float u;
@@ -1203,29 +1249,34 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
           }
         }
       }
+      iter = ui(iter);
+      S.sc[wv].iter = iter;
       const bool fin = iter >= a.max_iter;
       const bool can_check = ctm && iter > 0 && (iter % ctm == 0);
       const bool do_rho = interval && iter > 0 && (iter % interval == 0);
       if (!(can_check || do_rho || fin)) continue;
       float o[6], r[6];
       residuals(o, r, do_rho);
+      const float cinv = uf(S.sc[wv].cinv), qn0 = uf(S.sc[wv].qn0);
       const float pri_res = o[0], dua_res = cinv * o[3];
       if (can_check) {
         const float eps_p = a.eps_abs + a.eps_rel * fmaxf(o[1], o[2]);
-        const float eps_d = a.eps_abs + a.eps_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
+        const float eps_d = a.eps_abs + a.eps_rel * cinv * fmaxf(fmaxf(qn0, o[4]), o[5]);
         if (pri_res < eps_p && dua_res < eps_d) {
-          status = QLOCO_OK;
+          S.sc[wv].status = QLOCO_OK;
           break;
         }
       }
       if (do_rho) {  // compute_rho_estimate + adapt_rho
         const float pn = r[0] / (fmaxf(r[1], r[2]) + 1e-30f);
-        const float dn = r[3] / (fmaxf(fmaxf(qn[1], r[4]), r[5]) + 1e-30f);
+        const float dn = r[3] / (fmaxf(fmaxf(uf(S.sc[wv].qn1), r[4]), r[5]) + 1e-30f);
+        const float rho = uf(S.sc[wv].rho);
         float rho_new = rho * sqrtf(pn / (dn + 1e-30f));
         rho_new = fminf(fmaxf(rho_new, 1e-6f), 1e6f);
         if (rho_new > rho * a.rho_tol || rho_new < rho / a.rho_tol) {
-          rho = sgpr_f(rho_new);
-          rho_updates++;
+          const int nup = ui(S.sc[wv].rho_updates) + 1;
+          S.sc[wv].rho = sgpr_f(rho_new);
+          S.sc[wv].rho_updates = nup;
           if (!fin) {
             refactor = true;
             break;
@@ -1236,9 +1287,9 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
         float e_abs = a.eps_abs, e_rel = a.eps_rel;  // laundered: 10 eps is not hoisted into VGPRs
         asm volatile("" : "+v"(e_abs), "+v"(e_rel));
         const float ep = 10.f * e_abs + 10.f * e_rel * fmaxf(o[1], o[2]);
-        const float ed = 10.f * e_abs + 10.f * e_rel * cinv * fmaxf(fmaxf(qn[0], o[4]), o[5]);
-        status = __builtin_amdgcn_readfirstlane((pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE
-                                                                                 : QLOCO_MAX_ITER);
+        const float ed = 10.f * e_abs + 10.f * e_rel * cinv * fmaxf(fmaxf(qn0, o[4]), o[5]);
+        S.sc[wv].status = __builtin_amdgcn_readfirstlane((pri_res < ep && dua_res < ed) ? QLOCO_SOLVED_INACCURATE
+                                                                                          : QLOCO_MAX_ITER);
         break;
       }
     }
@@ -1250,10 +1301,16 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
   const int tid_o = W == 1 ? lane_o : (int)threadIdx.x;
   float xu[2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) xu[h] = valid[h] ? x[h] * Dr[h] : 0.0f;
+  for (int h = 0; h < 2; ++h) xu[h] = valid[h] ? x[h] * S.dr[wv][h][lane_o] : 0.0f;
+  // P~ x at the final iterate, recomputed (the last check's copy would be a
+  // register live across every ADMM iteration; same operands, same result)
+  float px[2];
+  p_times_x(px);
+  const float cinv = uf(S.sc[wv].cinv);
+  int status = ui(S.sc[wv].status);
   float ob = 0.0f;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) ob += valid[h] ? cinv * (0.5f * x[h] * px[h] + qv[h] * x[h]) : 0.0f;
+  for (int h = 0; h < 2; ++h) ob += valid[h] ? cinv * (0.5f * x[h] * px[h] + S.qvl[wv][h][lane_o] * x[h]) : 0.0f;
   const float objp = bsum<W>(S, wsum(ob), wv);
   const bool bad = !isfinite(objp);
   if (bad) status = QLOCO_NAN;
@@ -1281,7 +1338,8 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
   }
   if (prec) {  // the persistent record for the next call (layout QLOCO_SRBD_PERSIST_LEN)
     QL_LIT_LANE_INDICES(lxo);  // fresh indices: no address kept live from the warm start
-    for (int k = tid_o; k < NP + 4; k += 64 * W) prec[k] = 0.0f;
+    for (int k = tid_o; k < NP + 4; k += 64 * W)
+      if (k < 84 * N || k >= 96 * N) prec[k] = 0.0f;  // [84 N, 96 N): q, written at the gradient
     __syncthreads();
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1289,7 +1347,6 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       const int vidx = 12 * step[h] + 3 * leg[h] + comp, rbase = 20 * step[h] + 5 * leg[h] + 2 * comp;
       prec[vidx] = x[h];
       prec[52 * N + vidx] = xu[h];
-      prec[84 * N + vidx] = q_raw[h];
       prec[12 * N + rbase] = z[h].x;
       prec[32 * N + rbase] = y[h].x;
       const f2v e = row_e(h);
@@ -1302,7 +1359,7 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
     }
     for (int k = tid_o; k < 4 * N; k += 64 * W) prec[96 * N + k] = S.ctf[k];
     if (tid_o == 0) {
-      prec[NP] = rho;
+      prec[NP] = S.sc[wv].rho;
       prec[NP + 1] = 1.0f;
     }
   }
@@ -1325,8 +1382,8 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
   }
   if (tid_o == 0) {
     if (a.status) a.status[b] = status;
-    if (a.iters) a.iters[b] = iter;
-    if (a.rho_updates) a.rho_updates[b] = rho_updates;
+    if (a.iters) a.iters[b] = S.sc[wv].iter;
+    if (a.rho_updates) a.rho_updates[b] = S.sc[wv].rho_updates;
     if (a.obj) a.obj[b] = objp;
   }
 }
