@@ -246,6 +246,27 @@ int qloco_force_qp_solve(const qloco_force_params *prm, int64_t batch, const dou
                          int32_t *qp_solution, int32_t *status, int32_t *iters,
                          void *stream);
 
+/* The same solve with the robots grouped by control flow before the launch
+ * (swing-leg pattern, then the robot's previous active-set iteration count):
+ * the four robots that share a wavefront then take the same path.  Results
+ * are bit-identical to qloco_force_qp_solve.  order_ws: device int32
+ * workspace of qloco_force_order_ws_len(batch) entries, allocated and
+ * zero-filled once by the caller and passed unchanged on every call -- like
+ * F_leg_ref / grf_opt it carries per-robot state between calls (the
+ * iteration counts that predict the next call's grouping); NULL = the
+ * ungrouped launch.  No allocation happens inside, so the call can be
+ * captured in a HIP graph. */
+int64_t qloco_force_order_ws_len(int64_t batch);
+int qloco_force_qp_solve_ordered(const qloco_force_params *prm, int64_t batch,
+                                 const double *com_des, const double *leg_des,
+                                 const double *F_force_des, const double *rfoot_des,
+                                 const double *lfoot_des, const double *base_p,
+                                 const double *feet_p, const double *FT_total_des,
+                                 const int32_t *mode, const int32_t *right_support,
+                                 const double *y_coef, double *F_leg_ref, double *grf_opt,
+                                 double *F_leg_guess, int32_t *qp_solution, int32_t *status,
+                                 int32_t *iters, int32_t *order_ws, void *stream);
+
 /* Joint torques tau = -J^T F + g_comp (stance) or PD (swing),
  * Dynamiccclass::compute_joint_torques (dynmics_compute.cpp:109-138), for
  * all 4 legs of B instances.  Jaco[B*4*9] col-major per leg, swing[B*4],

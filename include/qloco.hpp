@@ -150,6 +150,7 @@ class Dynamiccclass {
   double *d_com_, *d_leg_, *d_F_, *d_rf_, *d_lf_, *d_base_, *d_feet_, *d_FT_, *d_y_, *d_Fref_,
       *d_grf_, *d_guess_;
   int32_t *d_mode_, *d_rs_, *d_qps_, *d_st_, *d_it_;
+  int32_t *d_ord_;           // grouped-launch workspace (qloco_force_order_ws_len)
   double *d_jt_ = nullptr;   // joint-torque staging (allocated on first use)
   int32_t *d_sw_ = nullptr;
 };

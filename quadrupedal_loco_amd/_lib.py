@@ -80,6 +80,8 @@ SIGNATURES = {
     "qloco_srbd_scratch_sets": (C.c_int, [C.c_void_p]),
     "qloco_force_params_default": (None, [C.POINTER(ForceParams)]),
     "qloco_force_qp_solve": (C.c_int, [C.POINTER(ForceParams), i64] + [vp] * 18),
+    "qloco_force_qp_solve_ordered": (C.c_int, [C.POINTER(ForceParams), i64] + [vp] * 19),
+    "qloco_force_order_ws_len": (i64, [i64]),
     "qloco_leg_fk": (C.c_int, [i64] + [vp] * 7),
     "qloco_leg_ik": (C.c_int, [i64] + [vp] * 10),
     "qloco_joint_torques": (C.c_int, [i64] + [vp] * 9),

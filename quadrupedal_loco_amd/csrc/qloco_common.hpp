@@ -7,6 +7,10 @@
 
 #define QLOCO_WAVE 64
 
+// grouped force-QP dispatch (qloco_force.hip): 5 swing-leg patterns x 16
+// iteration bins; the ordering workspace is 2 B + 2 kForceClasses int32
+#define QLOCO_FORCE_CLASSES 80
+
 namespace qloco {
 
 // thread-local last HIP error (qloco_last_error)

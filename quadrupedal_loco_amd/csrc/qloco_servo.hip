@@ -30,7 +30,7 @@ __constant__ double c_momentum[9] = {2 * 0.0168352186, 2 * 0.0004636141, 2 * 0.0
                                      2 * 0.0002367952, 2 * 3.6671e-05,   2 * 0.0742720659};
 
 struct Ws {  // byte offsets
-  int64_t fref, grf, guess, rel, rold, vrel, fsum, flr, swing, qps, st, total;
+  int64_t fref, grf, guess, rel, rold, vrel, fsum, flr, swing, qps, st, ord, total;
 };
 __host__ __device__ inline Ws layout(int64_t B) {
   auto al = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
@@ -46,7 +46,8 @@ __host__ __device__ inline Ws layout(int64_t B) {
   w.swing = al(w.flr + 8 * 6 * B);
   w.qps = al(w.swing + 4 * 4 * B);
   w.st = al(w.qps + 4 * B);
-  w.total = al(w.st + 4 * B);
+  w.ord = al(w.st + 4 * B);  // the force QP's grouping workspace (qloco_force_order_ws_len)
+  w.total = al(w.ord + 4 * (2 * B + 2 * QLOCO_FORCE_CLASSES));
   return w;
 }
 
@@ -199,12 +200,13 @@ extern "C" int qloco_servo_force_block(
   // rfoot_des, lfoot_des); Dynam.force_opt(body_p_des, FR..RL_foot_des, F_sum, gait_mode,
   // right_support, y_offset)  (:1216-1228)
   double *fref = (double *)(w + L.fref), *grf = (double *)(w + L.grf);
-  int rc = qloco_force_qp_solve(prm, batch, body_p_des, foot_des, (const double *)(w + L.flr),
-                                rfoot_des, lfoot_des, body_p_des, foot_des,
-                                (const double *)(w + L.fsum), gait_mode, right_support, y_offset,
-                                fref, grf, (double *)(w + L.guess),
-                                qp_solution ? qp_solution : (int32_t *)(w + L.qps),
-                                status ? status : (int32_t *)(w + L.st), nullptr, stream);
+  int rc = qloco_force_qp_solve_ordered(prm, batch, body_p_des, foot_des, (const double *)(w + L.flr),
+                                        rfoot_des, lfoot_des, body_p_des, foot_des,
+                                        (const double *)(w + L.fsum), gait_mode, right_support, y_offset,
+                                        fref, grf, (double *)(w + L.guess),
+                                        qp_solution ? qp_solution : (int32_t *)(w + L.qps),
+                                        status ? status : (int32_t *)(w + L.st), nullptr,
+                                        (int32_t *)(w + L.ord), stream);
   if (rc != QLOCO_OK) return rc;
   // compute_joint_torques for FR, FL, RR, RL (:1232-1243)
   rc = qloco_joint_torques(batch, Jaco, (const int32_t *)(w + L.swing), (const double *)(w + L.rel),

@@ -218,6 +218,10 @@ Dynamiccclass::Dynamiccclass(int batch, const qloco_force_params *params) : batc
   d_qps_ = dalloc<int32_t>(arena_, B);
   d_st_ = dalloc<int32_t>(arena_, B);
   d_it_ = dalloc<int32_t>(arena_, B);
+  // the grouped launch's workspace (previous iteration counts carried between calls)
+  const size_t nord = (size_t)qloco_force_order_ws_len(batch);
+  d_ord_ = dalloc<int32_t>(arena_, nord);
+  hip_ok(hipMemsetAsync(d_ord_, 0, sizeof(int32_t) * nord, (hipStream_t)arena_.stream()), "order workspace");
   // member state starts at zero (Dynamiccclass ctor, dynmics_compute.cpp:29-100)
   arena_.upload(d_Fref_, F_leg_ref.data(), sizeof(double) * B * 12);
   arena_.upload(d_grf_, grf_opt.data(), sizeof(double) * B * 12);
@@ -268,10 +272,10 @@ void Dynamiccclass::run() {
   arena_.upload(d_y_, h_y_.data(), sizeof(double) * B);
   arena_.upload(d_mode_, h_mode_.data(), sizeof(int32_t) * B);
   arena_.upload(d_rs_, h_rs_.data(), sizeof(int32_t) * B);
-  abi_ok(qloco_force_qp_solve(&prm_, batch_, d_com_, d_leg_, d_F_, d_rf_, d_lf_, d_base_, d_feet_,
-                              d_FT_, d_mode_, d_rs_, d_y_, d_Fref_, d_grf_, d_guess_, d_qps_,
-                              d_st_, d_it_, arena_.stream()),
-         "qloco_force_qp_solve");
+  abi_ok(qloco_force_qp_solve_ordered(&prm_, batch_, d_com_, d_leg_, d_F_, d_rf_, d_lf_, d_base_,
+                                      d_feet_, d_FT_, d_mode_, d_rs_, d_y_, d_Fref_, d_grf_, d_guess_,
+                                      d_qps_, d_st_, d_it_, d_ord_, arena_.stream()),
+         "qloco_force_qp_solve_ordered");
   arena_.download(grf_opt.data(), d_grf_, sizeof(double) * B * 12);
   arena_.download(F_leg_ref.data(), d_Fref_, sizeof(double) * B * 12);
   arena_.download(F_leg_guess.data(), d_guess_, sizeof(double) * B * 12);

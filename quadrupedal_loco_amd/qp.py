@@ -71,7 +71,7 @@ def force_params(**kw):
 class ForceQP:
     """Batched Dynamiccclass (force distribution QP) with device-resident state."""
 
-    def __init__(self, batch, device="cuda:0", **params):
+    def __init__(self, batch, device="cuda:0", grouped=True, **params):
         import torch
         self.batch = batch
         self.params = force_params(**params)
@@ -82,16 +82,20 @@ class ForceQP:
         self.qp_solution = torch.ones(batch, dtype=torch.int32, device=device)
         self.status = torch.zeros(batch, dtype=torch.int32, device=device)
         self.iters = torch.zeros(batch, dtype=torch.int32, device=device)
+        # grouping workspace (qloco_force_qp_solve_ordered): zero-filled once,
+        # carried between calls like the member state; None = ungrouped launch
+        self.order_ws = (torch.zeros(int(lib().qloco_force_order_ws_len(batch)), dtype=torch.int32,
+                                     device=device) if grouped else None)
 
     def step(self, com_des, leg_des, F_force_des, rfoot_des, lfoot_des, base_p, feet_p,
              FT_total_des, mode, right_support, y_coef):
         """servo.cpp:1224-1228: force_distribution(...) then force_opt(...)."""
-        check(lib().qloco_force_qp_solve(
+        check(lib().qloco_force_qp_solve_ordered(
             C.byref(self.params), self.batch, ptr(com_des), ptr(leg_des), ptr(F_force_des),
             ptr(rfoot_des), ptr(lfoot_des), ptr(base_p), ptr(feet_p), ptr(FT_total_des),
             ptr(mode), ptr(right_support), ptr(y_coef), ptr(self.F_leg_ref), ptr(self.grf_opt),
             ptr(self.F_leg_guess), ptr(self.qp_solution), ptr(self.status), ptr(self.iters),
-            _stream(com_des)), "qloco_force_qp_solve")
+            ptr(self.order_ws), _stream(com_des)), "qloco_force_qp_solve_ordered")
         return {"grf_opt": self.grf_opt, "F_leg_guess": self.F_leg_guess,
                 "F_leg_ref": self.F_leg_ref, "qp_solution": self.qp_solution,
                 "status": self.status, "iters": self.iters}

@@ -188,6 +188,13 @@ def test_rt_servo_support_argument_validation_without_device_work():
     assert L.qloco_servo_force_block(C.byref(fp), -1, *([None] * 22)) == 100
     assert L.qloco_servo_force_block(C.byref(fp), 0, *([None] * 22)) == 0
     assert L.qloco_servo_force_block(C.byref(fp), 4, *([None] * 22)) == 100
+    # the grouped force-QP launch: workspace length, argument checks
+    assert L.qloco_force_order_ws_len(-1) == -1
+    assert L.qloco_force_order_ws_len(1000) == 2 * 1000 + 160
+    assert L.qloco_force_qp_solve_ordered(None, 1, *([None] * 19)) == 100
+    assert L.qloco_force_qp_solve_ordered(C.byref(fp), -1, *([None] * 19)) == 100
+    assert L.qloco_force_qp_solve_ordered(C.byref(fp), 0, *([None] * 19)) == 0
+    assert L.qloco_force_qp_solve_ordered(C.byref(fp), 4, *([None] * 19)) == 100
 
 
 def test_srbd_polish_rejected_until_implemented():

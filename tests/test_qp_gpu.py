@@ -180,6 +180,39 @@ def test_force_qp_matches_restatement_over_ticks():
         O.lib().qo_dyn_free(C.byref(s))
 
 
+def test_force_qp_grouped_launch_is_bit_identical():
+    """qloco_force_qp_solve_ordered groups the robots by swing-leg pattern and
+    previous iteration count before the launch; every robot's
+    arithmetic is unchanged, so grf_opt / F_leg_ref / status / iterations equal
+    the ungrouped launch's bit for bit, tick after tick (the member state and
+    the grouping state both carried).  B = 1001: a partial last wavefront.
+    The workspace's list is a permutation in (pattern, previous iterations)
+    order."""
+    dev = _dev()
+    rng = np.random.default_rng(11)
+    B, ticks = 1001, 4
+    grouped = qp.ForceQP(batch=B, device=dev)
+    plain = qp.ForceQP(batch=B, device=dev, grouped=False)
+    assert grouped.order_ws.numel() == 2 * B + 160
+    for tick in range(ticks):
+        inp = force_inputs(rng, B)
+        d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in inp.items()}
+        prev = grouped.order_ws[:B].clone()
+        og = grouped.step(**d)
+        op = plain.step(**d)
+        torch.cuda.synchronize()
+        for k in ("grf_opt", "F_leg_guess", "F_leg_ref", "qp_solution", "status", "iters"):
+            assert torch.equal(og[k], op[k]), (tick, k)
+        assert torch.equal(grouped.order_ws[:B], op["iters"]), tick  # carried for the next call
+        lst = grouped.order_ws[B:2 * B].cpu().numpy()
+        assert np.array_equal(np.sort(lst), np.arange(B)), tick
+        m, rs = inp["mode"][lst], inp["right_support"][lst]
+        pat = np.where(m == 102, np.where(rs == 0, 1, np.where(rs == 1, 2, 0)),
+                       np.where(m == 101, np.where(rs == 0, 3, np.where(rs == 1, 4, 0)), 0))
+        key = pat * 16 + np.minimum(prev.cpu().numpy()[lst], 15)
+        assert np.all(np.diff(key) >= 0), tick
+
+
 def test_body_mpc_matches_restatement_over_a_gait():
     dev = _dev()
     rng = np.random.default_rng(11)

@@ -87,6 +87,11 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--order", choices=("given", "pattern", "iters"), default="given",
+                    help="experiment: permute the robots on the host before timing -- grouped by "
+                         "swing-leg pattern, or by pattern then by a first solve's iteration count")
+    ap.add_argument("--ungrouped", action="store_true",
+                    help="the plain launch (qloco_force_qp_solve) instead of the grouped one")
     ap.add_argument("--servo", action="store_true",
                     help="time the whole servo force block (qloco_servo_force_block)")
     args = ap.parse_args()
@@ -101,8 +106,19 @@ def main():
     B = args.robots
     dev = torch.device("cuda:0")
     inp = force_inputs(np.random.default_rng(3), B)
+    if args.order != "given":
+        m, rs = inp["mode"], inp["right_support"]
+        pat = np.where(m == 102, np.where(rs == 0, 1, np.where(rs == 1, 2, 0)),
+                       np.where(m == 101, np.where(rs == 0, 3, np.where(rs == 1, 4, 0)), 0))
+        key = pat.astype(np.int64) * 1000
+        if args.order == "iters":
+            d0 = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in inp.items()}
+            it0 = qp.ForceQP(batch=B, device=dev).step(**d0)["iters"].cpu().numpy()
+            key = key + it0
+        perm = np.argsort(key, kind="stable")
+        inp = {k: v[perm] for k, v in inp.items()}
     d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in inp.items()}
-    solver = qp.ForceQP(batch=B, device=dev)
+    solver = qp.ForceQP(batch=B, device=dev, grouped=not args.ungrouped)
     for _ in range(args.warmup):
         out = solver.step(**d)
     torch.cuda.synchronize()
@@ -125,7 +141,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms,
             "p99_batch_us": float(np.percentile(per, 99) * 1e3), "higher_is_better": True,
             "dtype": "f64", "data": "synthetic (tests/cases.force_inputs, seed 3)",
-            "config": {"workload": "force QP, %d robots, modes 101/102/103, right_support 0/1/2" % B},
+            "config": {"workload": "force QP, %d robots, modes 101/102/103, right_support 0/1/2%s%s" % (
+                B, "" if args.order == "given" else ", host order: " + args.order,
+                ", ungrouped launch" if args.ungrouped else ", grouped launch (pattern, previous iterations)")},
             "gi_iters_mean": float(iters.mean()), "status_ok_frac": float(np.mean(status == 0)),
             "roofline": {"bound": "valu-fp64", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS,
