@@ -86,7 +86,6 @@ struct SrbdLds {
   f4v zb[NC];               // per var: scaled bounds (l0, u0, l1, u1) of its 2 slots
   f4v arz[NC];              // per var: scaled A entries (ra0, ra1, rz0, rz1) of its 2 slots
   float qs[NC];             // per var: scaled q
-  float qss[NC];            // per var: Ruiz's running q for the cost scale (the record's q on the update path)
   int pair[NC];             // per var: 4*step + leg
   int cst[NC];              // per var: step, NM on padding (row of zeros in k0k2)
   f2v k0k2[NM * (NM + 1)];  // [row step][col step]: horizon sums K0, K2
@@ -756,15 +755,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
   // (Ruiz scales them in place; registers would carry them across the setup)
   S.arz[t] = (f4v){valid ? 1.0f : 0.0f, (valid && xy) ? 1.0f : 0.0f, (valid && xy) ? a.mu : 0.0f,
                    (valid && xy) ? -a.mu : 0.0f};
-  // Ruiz's per-variable state (D, E of the two rows, q, the cost-scale q)
-  // lives in LDS through the passes: registers would carry it across the
-  // P row (the two-wave buckets' spill point)
-  float cs = 1.0f;
-  S.Dc[t] = 1.0f;
-  S.aux[1][t] = 1.0f;
-  S.aux[2][t] = 1.0f;
-  S.qs[t] = qv;
-  S.qss[t] = qsv;
+  float rE0 = 1.0f, rE1 = 1.0f, Dr = 1.0f, cs = 1.0f;
   S.aux[0][t] = r2v;
   S.pair[t] = 4 * step + leg;
 
@@ -890,12 +881,11 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         rz0 *= Et0 * Dz;
         rz1 *= Et1 * Dz;
         S.arz[t] = (f4v){ra0, ra1, rz0, rz1};
-        S.aux[1][t] *= Et0;
-        S.aux[2][t] *= Et1;
-        S.qs[t] *= Dt;
-        const float qsv = S.qss[t] * Dt;
-        const float Dr = S.Dc[t] * Dt;
-        S.Dc[t] = Dr;
+        rE0 *= Et0;
+        rE1 *= Et1;
+        qv *= Dt;
+        qsv *= Dt;
+        Dr *= Dt;
         const int buf = it & 1;
         reinterpret_cast<float *>(&S.bc[buf][0])[t] = Dr;
         bsync<W>();
@@ -922,8 +912,8 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         const float meanP = cs * sumP * inv_n;
         // v_rcp_f32 (1 ulp), like the rsq above: a heuristic factor
         const float ctc = __builtin_amdgcn_rcpf(limit_scaling(fmaxf(meanP, limit_scaling(qm[0]))));
-        S.qs[t] *= ctc;
-        S.qss[t] = qsv * ctc;
+        qv *= ctc;
+        qsv *= ctc;
         cs *= ctc;
         cnP = cn2 * cs;
       }
@@ -934,7 +924,6 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       const float cflag = valid ? (float)S.ct[S.pair[opaque_tid()]] : 0.0f;
       const float rl0 = !valid ? 0.0f : (xy ? 0.0f : a.fz_min * cflag);
       const float ru0 = !valid ? 0.0f : (xy ? INFINITY : a.fz_max * cflag);
-      const float rE0 = S.aux[1][t], Dr = S.Dc[t], qv = S.qs[t];
       const float lh0 = rl0 * rE0, uh0 = ru0 * rE0;
       // slot 1: (-inf, 0] on x/y lanes (E scaling keeps 0 and inf), inert [0, 0] elsewhere
       const float lh1 = (valid && xy) ? -INFINITY : 0.0f, uh1 = 0.0f;
@@ -943,6 +932,9 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
       // no row is loose.  The inert slot-1 rows have a zero A row, so their rho
       // never matters -- rho vector = (eq0 ? 1e3 rho : rho, rho).
       eq0 = valid && !xy && (uh0 - lh0 < 1e-4f);
+      S.Dc[t] = valid ? Dr : 1.0f;
+      S.aux[1][t] = rE0;
+      S.aux[2][t] = rE1;
       S.zb[t] = (f4v){lh0, uh0, lh1, uh1};
       // ||D^-1 q||_inf and ||q||_inf (scaled) are constant over the iterations
       float qn[2] = {fabsf(qv / Dr), fabsf(qv)};
@@ -951,6 +943,7 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         S.qn[0] = qn[0];
         S.qn[1] = qn[1];
       }
+      S.qs[t] = qv;
       bsync<W>();
     }
     // ---------------- 8. K = cs D P D + sigma I + A' rho A, inverse in registers
@@ -993,9 +986,9 @@ __device__ __forceinline__ void srbd_solve_one(const SrbdArgs &a, SrbdLds<W, NM>
         // + setPrimal/DualVariable)
         const float *wx = a.warm_start == 1 ? a.warm + b * (32 * N) : prec + 52 * N;
         const float *wy = wx + 12 * N;
-        x = valid ? wx[vidx] / S.Dc[tf] : 0.0f;
-        y.x = valid ? wy[rbase] / S.aux[1][tf] * cs : 0.0f;
-        y.y = (valid && xy) ? wy[rbase + 1] / S.aux[2][tf] * cs : 0.0f;
+        x = valid ? wx[vidx] / Dr : 0.0f;
+        y.x = valid ? wy[rbase] / rE0 * cs : 0.0f;
+        y.y = (valid && xy) ? wy[rbase + 1] / rE1 * cs : 0.0f;
         const float n1 = lane_next(x), n2 = lane_next(n1);
         const float xz = comp == 0 ? n2 : (comp == 1 ? n1 : x);
         const f4v arz = S.arz[t];

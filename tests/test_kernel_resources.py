@@ -21,7 +21,8 @@ READELF = shutil.which("llvm-readelf", path="/opt/rocm/lib/llvm/bin:/opt/rocm/ll
 
 # spilled VGPRs allowed (upper bounds, the round-4 build)
 SPILL_BOUND = {
-    "_ZN5qloco16srbd_admm_kernelILi2ELi3ELb0ELi20ELi15EEEvNS_8SrbdArgsE": 16,   # C2 = 15 bucket
+    "_ZN5qloco16srbd_admm_kernelILi1ELi4ELb1ELi10ELi16EEEvNS_8SrbdArgsE": 1,    # warm-start one-wave
+    "_ZN5qloco16srbd_admm_kernelILi2ELi3ELb0ELi20ELi15EEEvNS_8SrbdArgsE": 33,   # C2 = 15 bucket
     "_ZN5qloco20srbd_admm_big_kernelILb1ELi128EEEvNS_8SrbdArgsE": 34,           # warm wide kernel
     "_ZN5qloco20srbd_admm_big_kernelILb0ELi120EEEvNS_8SrbdArgsE": 3,
 }

@@ -98,6 +98,11 @@ def run(B, gait, shuffle=False):
         print("   per-wave solve us: p50 %.1f p99 %.1f max %.1f;  per-SIMD iterations sum min %d p50 %d max %d" % (
             *np.percentile(s1 - s0, [50, 99, 100]), itsum.min(), np.median(itsum), itsum.max()))
         if r == 0:
+            # dispatch placement: do the instances sharing a SIMD follow i mod (number of SIMDs)?
+            nsimd = len(keys)
+            same = np.mean([len(set((np.nonzero(inv == k)[0] % nsimd).tolist())) == 1 for k in range(nsimd)])
+            print("   placement: %.3f of SIMDs hold instances with one value of i mod %d; "
+                  "SIMD key of instances 0..7: %s" % (same, nsimd, key[:8].tolist()))
             late = np.argsort(-end)[:3]
             for k in late:
                 sel = inv == k
