@@ -333,15 +333,18 @@ def main():
                 pending[k].wait()
                 pending[k] = None
 
-    # Side measurements (one GPU) run BEFORE the headline's warm-up: the
+    # Side measurements run BEFORE the headline's warm-up: the
     # headline is then timed at the clocks a continuously running controller
     # sees.  A cold GPU ramps its clocks over the first ~40 launches (554 us
     # per launch over the first 20, 515 us from launch 40 on,
     # profiles/r5a_step_timeline.txt), so W = 5 warm-up steps alone would time
     # part of the ramp.  The timed region itself is unchanged:
     # exactly K steps of the full solve, W untimed steps before it.
+    # Every rank runs the two rank-local lines (its own shard, no collective),
+    # so an N-GPU run times its headline at the same clocks as the 1-GPU run;
+    # the line printed is rank 0's.
     side = {}
-    if rank == 0 and world == 1 and not args.no_second_line:
+    if not args.no_second_line:
         key = "reduced_qp" if args.literal else "literal_full_qp"
         side[key] = second_line(args, srbd, d_x0, d_xr, d_ft, d_ct, ct, stream, dev, not args.literal)
         try:  # side measurements: never lose the headline line over one
@@ -349,6 +352,7 @@ def main():
                                                    args.literal)
         except Exception as e:  # noqa: BLE001
             side["shuffled_order"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_second_line:
         if args.horizon <= 20:
             try:
                 side["persistent_literal"] = steady_line(args, srbd, stream, dev)
