@@ -151,6 +151,28 @@ int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, const float 
                         int32_t *rho_updates, float *obj, float *warm,
                         int32_t max_stance_legs, void *stream);
 
+/* The kernel family a qloco_srbd_solve[_ex] call with this spec runs
+ * (host-only, no device work; the solve uses the same decision):
+ *   QLOCO_ROUTE_LIT_ONE_WAVE  literal QP, N <= 10: srbd_lit_kernel (one wavefront
+ *                             per instance, the OSQP solve through the wrench space)
+ *   QLOCO_ROUTE_LIT_TWO_WAVE  literal QP, N = 11..20, state weights <= 1000:
+ *                             srbd_lit2_kernel
+ *   QLOCO_ROUTE_LIT_GENERIC   literal QP otherwise (a q_omega / q_v weight of 0,
+ *                             per-step feet, N > 20, or N > 10 with a state
+ *                             weight above 1000): the 12N-variable kernels
+ *   QLOCO_ROUTE_REDUCED       literal_full_qp = 0: the stance-only classes
+ * At N <= 10 any q_weights with q_omega, q_v > 0 -- the Go1 defaults and all
+ * three of the reference's config/{gazebo,hardware,isaac}_a1_mpc.yaml sets,
+ * isaac's anisotropic omega weights included -- take the one-wave
+ * wrench-space kernel; at N = 11..20 the Go1 / gazebo / hardware sets take
+ * the two-wave one and isaac's (roll 8000) the generic kernels (the two-wave
+ * kernel's float32 solve).  Returns QLOCO_ERR_ARG on a bad spec. */
+#define QLOCO_ROUTE_LIT_ONE_WAVE 1
+#define QLOCO_ROUTE_LIT_TWO_WAVE 2
+#define QLOCO_ROUTE_LIT_GENERIC 3
+#define QLOCO_ROUTE_REDUCED 4
+int qloco_srbd_route(const qloco_srbd_spec *spec);
+
 /* Class-dispatch scratch of qloco_srbd_solve_ex (instance lists, counters,
  * side streams, events): one set per (device, caller stream), at most 8
  * live -- the least recently used set beyond that is released.  Returns the
@@ -266,6 +288,22 @@ int qloco_force_qp_solve_ordered(const qloco_force_params *prm, int64_t batch,
                                  const double *y_coef, double *F_leg_ref, double *grf_opt,
                                  double *F_leg_guess, int32_t *qp_solution, int32_t *status,
                                  int32_t *iters, int32_t *order_ws, void *stream);
+
+/* The hardware servo's Dynamiccclass constants (unitree_legged_real copy of
+ * dynmics_compute.cpp:31,65: mass = gait::mass = 14, robot_const_para_config
+ * .cpp:28; mu = 0.5), the call at torque_mode.cpp:1364-1367; the other
+ * fields as qloco_force_params_default (the sim copy: mass 12, mu 0.25). */
+void qloco_force_params_hw(qloco_force_params *p);
+
+/* The hardware loop's feed-forward after force_opt (unitree_legged_real
+ * torque_mode.cpp:1370-1384): rate = min((dynamic_count / 500)^2, 1),
+ * F_opt = rate (grf_opt - grf_base) + grf_base per leg (grf_base: the
+ * stand-up FR_GRF .. RL_GRF of :1057-1058), tau = -J^T F_opt -- no gravity
+ * compensation.  Per instance: Jaco[4*9] (col-major per leg), grf_opt[12],
+ * grf_base[12], dynamic_count (int32) -> tau[12]; legs FR, FL, RR, RL. */
+int qloco_hw_torque_ff(int64_t batch, const double *Jaco, const double *grf_opt,
+                       const double *grf_base, const int32_t *dynamic_count, double *tau,
+                       void *stream);
 
 /* Joint torques tau = -J^T F + g_comp (stance) or PD (swing),
  * Dynamiccclass::compute_joint_torques (dynmics_compute.cpp:109-138), for

@@ -222,6 +222,30 @@ void qo_compute_joint_torques(const qo_dyn_state *s, const double J[9], int swin
   }
 }
 
+/* The hardware loop's feed-forward after force_opt (unitree_legged_real
+ * torque_mode.cpp:1370-1384): the stand-up ramp rate = min((dynamic_count /
+ * 500)^2, 1) blends each leg's grf_opt with the leg's stand-up GRF (FR_GRF ..
+ * RL_GRF, set at :1057-1058), then Torque_ff_GRF = -J' F_opt per leg -- no
+ * gravity compensation (the sim's compute_joint_torques adds it).  Legs in the
+ * servo order FR, FL, RR, RL; J 3x3 col-major per leg; the product summed in
+ * compute_joint_torques' order. */
+void qo_hw_torque_ff(const double Jaco[36], const double grf_opt[12], const double grf_base[12],
+                     int32_t dynamic_count, double tau[12]) {
+  double rate = pow(dynamic_count / 500.0, 2); /* :1370 */
+  if (rate >= 1) rate = 1;                     /* :1371-1374 */
+  for (int l = 0; l < 4; ++l) {
+    double f[3];
+    for (int k = 0; k < 3; ++k)
+      f[k] = (rate * (grf_opt[3 * l + k] - grf_base[3 * l + k])) + grf_base[3 * l + k]; /* :1376-1379 */
+    const double *J = Jaco + 9 * l;
+    for (int r = 0; r < 3; ++r) {
+      double acc = 0.0;
+      for (int k = 0; k < 3; ++k) acc += J[r * 3 + k] * f[k];
+      tau[3 * l + r] = -acc; /* :1381-1384 */
+    }
+  }
+}
+
 /* Batch driver for the CPU baseline (tools/bench_qp.py): servo.cpp:1224-1228
  * (force_distribution then force_opt) for n robots, row layout of
  * qloco_force_qp_solve, one persistent Dynamiccclass per robot in `states`

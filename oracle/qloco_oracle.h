@@ -96,6 +96,10 @@ void qo_force_batch(int64_t n, qo_dyn_state *states, const qo_force_params *prm,
                     const double *rfoot_des, const double *lfoot_des, const double *base_p,
                     const double *feet_p, const double *FT_total_des, const int32_t *mode,
                     const int32_t *right_support, const double *y_coef, double *grf_opt);
+/* unitree_legged_real torque_mode.cpp:1370-1384 (hardware feed-forward):
+ * ramp-blended grf_opt, tau = -J' F per leg, legs FR, FL, RR, RL */
+void qo_hw_torque_ff(const double Jaco[36], const double grf_opt[12], const double grf_base[12],
+                     int32_t dynamic_count, double tau[12]);
 /* dynmics_compute.cpp:109-138; Jaco 3x3 col-major; swing_flag = `support_flag` */
 void qo_compute_joint_torques(const qo_dyn_state *s, const double Jaco[9],
                               int swing_flag, const double p_des[3],

@@ -62,6 +62,7 @@ SIGNATURES = {
     "qloco_last_error": (C.c_char_p, []),
     "qloco_srbd_spec_default": (None, [C.POINTER(SrbdSpec)]),
     "qloco_srbd_max_stance_vars": (C.c_int, []),
+    "qloco_srbd_route": (C.c_int, [C.POINTER(SrbdSpec)]),
     "qloco_srbd_solve": (C.c_int, [C.POINTER(SrbdSpec), i64, vp, vp, vp, vp, vp, vp, vp, vp,
                                    vp, vp, vp]),
     "qloco_srbd_solve_ex": (C.c_int, [C.POINTER(SrbdSpec), i64, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -85,6 +86,8 @@ SIGNATURES = {
     "qloco_leg_fk": (C.c_int, [i64] + [vp] * 7),
     "qloco_leg_ik": (C.c_int, [i64] + [vp] * 10),
     "qloco_joint_torques": (C.c_int, [i64] + [vp] * 9),
+    "qloco_force_params_hw": (None, [C.POINTER(ForceParams)]),
+    "qloco_hw_torque_ff": (C.c_int, [i64] + [vp] * 6),
     "qloco_body_state_init_host": (C.c_int, [i64, vp]),
     "qloco_body_mpc_step": (C.c_int, [i64] + [vp] * 10),
     "qloco_body_indexfind": (C.c_int, [i64, vp, vp, vp]),

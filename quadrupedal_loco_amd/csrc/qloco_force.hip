@@ -339,9 +339,54 @@ __global__ void joint_torque_kernel(int64_t batch, const double *Jaco, const int
   }
 }
 
+// unitree_legged_real torque_mode.cpp:1370-1384 (the hardware loop after
+// force_opt), one thread per (instance, leg): the stand-up ramp blends
+// grf_opt with the leg's stand-up GRF, tau_ff = -J' F_opt, no gravity
+// compensation; the product summed in joint_torque_kernel's order
+__global__ void hw_torque_ff_kernel(int64_t batch, const double *Jaco, const double *grf_opt,
+                                    const double *grf_base, const int *dynamic_count, double *tau) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= batch * 4) return;
+  const int64_t inst = t >> 2;
+  const double x = dynamic_count[inst] / 500.0;
+  double rate = x * x;  // pow(x, 2), :1370 (both correctly rounded)
+  if (rate >= 1) rate = 1;
+  const double *J = Jaco + t * 9;
+  double f[3];
+  for (int k = 0; k < 3; ++k) {
+    const double b = grf_base[t * 3 + k];
+    f[k] = (rate * (grf_opt[t * 3 + k] - b)) + b;
+  }
+  for (int r = 0; r < 3; ++r) {
+    double acc = 0.0;
+    for (int k = 0; k < 3; ++k) acc += J[r * 3 + k] * f[k];
+    tau[t * 3 + r] = -acc;
+  }
+}
+
 }  // namespace qloco
 
 using namespace qloco;
+
+extern "C" void qloco_force_params_default(qloco_force_params *p);
+extern "C" void qloco_force_params_hw(qloco_force_params *p) {
+  qloco_force_params_default(p);
+  p->mass = 14.0;  // gait::mass, unitree_legged_real robot_const_para_config.cpp:28 (dynmics_compute.cpp:31)
+  p->mu = 0.5;     // unitree_legged_real dynmics_compute.cpp:65
+}
+
+extern "C" int qloco_hw_torque_ff(int64_t batch, const double *Jaco, const double *grf_opt,
+                                  const double *grf_base, const int32_t *dynamic_count, double *tau,
+                                  void *stream) {
+  if (batch < 0 || (batch > 0 && (!Jaco || !grf_opt || !grf_base || !dynamic_count || !tau)))
+    return QLOCO_ERR_ARG;
+  if (batch == 0) return QLOCO_OK;
+  const int64_t threads = batch * 4;
+  hipLaunchKernelGGL(hw_torque_ff_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, batch, Jaco, grf_opt, grf_base, (const int *)dynamic_count, tau);
+  QLOCO_HIP_CHECK(hipGetLastError(), "hw_torque_ff_kernel launch");
+  return QLOCO_OK;
+}
 
 extern "C" void qloco_force_params_default(qloco_force_params *p) {
   p->mass = 12.0;

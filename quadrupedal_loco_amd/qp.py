@@ -60,12 +60,38 @@ def eiquadprog_solve(G, g0, CE, ce0, CI, ci0, n, p, m):
     return out
 
 
-def force_params(**kw):
+def force_params(hw=False, **kw):
+    """Dynamiccclass constants: the sim copy (go1_rt_control
+    dynmics_compute.cpp:29-100, mass 12, mu 0.25) or, hw=True, the hardware
+    copy the torque-mode loop uses (unitree_legged_real: mass = gait::mass
+    = 14, mu = 0.5; qloco_force_params_hw)."""
     p = ForceParams()
-    lib().qloco_force_params_default(C.byref(p))
+    (lib().qloco_force_params_hw if hw else lib().qloco_force_params_default)(C.byref(p))
     for k, v in kw.items():
         setattr(p, k, v)
     return p
+
+
+def hw_torque_ff(Jaco, grf_opt, grf_base, dynamic_count, stream=None):
+    """The hardware loop's joint feed-forward after force_opt
+    (unitree_legged_real torque_mode.cpp:1370-1384): stand-up ramp
+    rate = min((dynamic_count / 500)^2, 1), F = rate (grf_opt - grf_base) +
+    grf_base per leg, tau = -J^T F (no gravity compensation).  Jaco (B, 4, 9)
+    col-major per leg, grf_opt / grf_base (B, 12) float64, dynamic_count (B,)
+    int32; legs FR, FL, RR, RL.  Returns tau (B, 12) float64."""
+    import torch
+    B = grf_opt.shape[0]
+    for name, t, dt, n in (("Jaco", Jaco, torch.float64, 36), ("grf_opt", grf_opt, torch.float64, 12),
+                           ("grf_base", grf_base, torch.float64, 12),
+                           ("dynamic_count", dynamic_count, torch.int32, 1)):
+        if t.dtype != dt or not t.is_contiguous() or not t.is_cuda or t.numel() != B * n:
+            raise ValueError("%s: need a contiguous %s device tensor with %d entries per instance"
+                             % (name, dt, n))
+    tau = torch.empty((B, 12), dtype=torch.float64, device=grf_opt.device)
+    check(lib().qloco_hw_torque_ff(B, ptr(Jaco), ptr(grf_opt), ptr(grf_base), ptr(dynamic_count),
+                                   ptr(tau), C.c_void_p(stream) if stream is not None else _stream(grf_opt)),
+          "qloco_hw_torque_ff")
+    return tau
 
 
 class ForceQP:

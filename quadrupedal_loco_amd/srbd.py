@@ -22,6 +22,28 @@ from ._lib import SrbdSpec, check, lib, ptr
 
 GAITS = {"trot": 0, "pace": 1, "biped": 1, "mixed": 2, "stance": 3}
 
+# The MPC weight sets the reference ships, loaded by a1_ctrl.launch by `type`
+# (unitree_ros/a1_cpp_open_source/config/{gazebo,hardware,isaac}_a1_mpc.yaml,
+# q_weights_0..12 and r_weights_0..11; A1CtrlStates.h:193-230 reads them).
+# isaac's omega weights are anisotropic (q_omega_x 20.05 != q_omega_y 30.05).
+REFERENCE_WEIGHTS = {
+    "gazebo": ([20.0, 10.0, 1.0, 0.0, 0.0, 420.0, 0.05, 0.05, 0.05, 30.0, 30.0, 10.0, 0.0],
+               [1e-7] * 12),
+    "hardware": ([150.0, 150.0, 50.0, 0.0, 0.0, 80.0, 0.2, 0.2, 0.2, 0.3, 0.3, 0.3, 0.0],
+                 [1e-5, 1e-5, 1e-6] * 3 + [1e-6] * 3),
+    "isaac": ([8000.0, 4000.0, 3000.0, 0.0, 0.0, 6020.0, 20.05, 30.05, 0.05, 2130.0, 2130.0, 110.0, 0.0],
+              [1e-5, 1e-5, 1e-6] * 4),
+}
+
+
+def route(spec):
+    """The kernel family qloco_srbd_solve runs for `spec` (qloco_srbd_route):
+    1 literal one-wave, 2 literal two-wave, 3 literal generic, 4 reduced."""
+    r = lib().qloco_srbd_route(C.byref(spec))
+    if r >= 100:
+        check(r, "qloco_srbd_route")
+    return r
+
 
 def default_spec(**overrides):
     """Go1 constants + OSQP default settings."""
@@ -130,14 +152,13 @@ def check_inputs(spec, x0, x_ref, feet, contacts, warm=None, device=None):
     B = x0.shape[0]
     N = int(spec.horizon)
     dev = torch.device(device) if device is not None else x0.device
-    for name, t, dt in (("x0", x0, torch.float32), ("x_ref", x_ref, torch.float32),
-                        ("feet", feet, torch.float32), ("contacts", contacts, torch.uint8)):
+    # layout checks first, device placement last: every layout error is
+    # reported as itself whatever device the tensors are on
+    named = (("x0", x0, torch.float32), ("x_ref", x_ref, torch.float32),
+             ("feet", feet, torch.float32), ("contacts", contacts, torch.uint8))
+    for name, t, dt in named:
         if t.dtype != dt or not t.is_contiguous() or t.dim() != 2 or t.shape[0] != B:
             raise ValueError("%s: need a contiguous 2-D %s tensor with batch %d" % (name, dt, B))
-        if not t.is_cuda:
-            raise ValueError("%s must be a device tensor (inputs resident in HBM)" % name)
-        if t.device != dev:
-            raise ValueError("%s is on %s, expected %s" % (name, t.device, dev))
     if x0.shape[1] != 13 or x_ref.shape[1] != 13 * N:
         raise ValueError("x0 (B,13) and x_ref (B,13N) expected")
     if feet.shape[1] not in (12, 12 * N):
@@ -150,9 +171,15 @@ def check_inputs(spec, x0, x_ref, feet, contacts, warm=None, device=None):
     if wl:
         if warm is None:
             raise ValueError("warm_start %d needs a warm buffer (B, %d)" % (spec.warm_start, wl))
-        if (warm.dtype != torch.float32 or not warm.is_contiguous() or not warm.is_cuda
-                or warm.device != dev or warm.numel() != B * wl or warm.shape[0] != B):
+        if (warm.dtype != torch.float32 or not warm.is_contiguous()
+                or warm.numel() != B * wl or warm.shape[0] != B):
             raise ValueError("warm: need a contiguous float32 (%d, %d) tensor on %s" % (B, wl, dev))
+        named = named + (("warm", warm, torch.float32),)
+    for name, t, _ in named:
+        if not t.is_cuda:
+            raise ValueError("%s must be a device tensor (inputs resident in HBM)" % name)
+        if t.device != dev:
+            raise ValueError("%s is on %s, expected %s" % (name, t.device, dev))
 
 
 class BatchedConvexMpc:

@@ -139,6 +139,7 @@ def lib():
                                    dp, dp, dp, C.c_int, C.c_int, C.c_double, ip, ip]
         L.qo_compute_joint_torques.argtypes = [C.POINTER(DynState), dp, C.c_int, dp, dp, dp,
                                                dp, C.c_int, dp]
+        L.qo_hw_torque_ff.argtypes = [dp, dp, dp, C.c_int32, dp]
         L.qo_body_init.argtypes = [C.POINTER(BodyState)]
         L.qo_body_free.argtypes = [C.POINTER(BodyState)]
         L.qo_body_indexfind.restype = C.c_int

@@ -139,7 +139,9 @@ def test_solve_refuses_bad_tensors_before_the_c_call():
     """MgpuSolver.solve ran no input checks, so a CPU, float64 or
     non-contiguous tensor reached qloco_mgpu_solve as a bad device pointer.
     Both entry points now share srbd.check_inputs; every case below raises
-    ValueError on the host (no GPU needed, no C call made)."""
+    ValueError on the host (no GPU needed, no C call made), and
+    each with its own check's message: layout checks run before the device
+    check, so CPU tensors still reach the feet / x_ref / contacts checks."""
     from quadrupedal_loco_amd import srbd
     B, Nh = 4, 10
     spec = srbd.default_spec(horizon=Nh)
@@ -151,16 +153,17 @@ def test_solve_refuses_bad_tensors_before_the_c_call():
     h.spec, h.count, h.device, h._h = spec, B, torch.device("cuda", 0), None
     solver = srbd.BatchedConvexMpc(spec=spec)
     bad = [
-        (x0, xr, ft, ct),                                      # CPU tensors
-        (x0.double(), xr, ft, ct),                             # float64
-        (x0, xr, torch.zeros((B, 24), dtype=torch.float32).t().contiguous().t()[:, :12], ct),
-        (x0, xr[:, :13 * Nh - 1], ft, ct),                     # x_ref width
-        (x0, xr, ft, ct.to(torch.int32)),                      # contacts dtype
+        ((x0, xr, ft, ct), "x0 must be a device tensor"),                 # CPU tensors
+        ((x0.double(), xr, ft, ct), "x0: need a contiguous"),             # float64
+        ((x0, xr, torch.zeros((B, 24), dtype=torch.float32).t().contiguous().t()[:, :12], ct),
+         "feet: need a contiguous"),                                      # non-contiguous feet
+        ((x0, xr[:, :13 * Nh - 1].contiguous(), ft, ct), r"x_ref \(B,13N\)"),  # x_ref width
+        ((x0, xr, ft, ct.to(torch.int32)), "contacts: need a contiguous"),  # contacts dtype
     ]
-    for args in bad:
-        with pytest.raises(ValueError):
+    for args, msg in bad:
+        with pytest.raises(ValueError, match=msg):
             h.solve(*args)
-        with pytest.raises(ValueError):
+        with pytest.raises(ValueError, match=msg):
             solver.solve(*args)
     with pytest.raises(ValueError):  # this rank's instance count
         h.solve(x0[:2], xr[:2], ft[:2], ct[:2])

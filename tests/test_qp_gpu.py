@@ -133,18 +133,28 @@ def test_eiquadprog_wide_matches_restatement(n, p, m, zero_ce):
     assert np.mean(it) > 2  # the active set did work
 
 
-def test_force_qp_matches_restatement_over_ticks():
+@pytest.mark.parametrize("hw,grouped", [(False, False), (True, True), (True, False)])
+def test_force_qp_matches_restatement_over_ticks(hw, grouped):
+    """force_distribution + force_opt over three ticks of member state against
+    the oracle (dynmics_compute.cpp:141-445), bit-exact in >= 90 % of
+    instances and within 1e-9 otherwise -- with the sim's constants (mass 12,
+    mu 0.25) and with the hardware copy's (unitree_legged_real: mass =
+    gait::mass = 14, mu = 0.5, called at torque_mode.cpp:1364-1367), through
+    the plain and the grouped launch."""
     dev = _dev()
     rng = np.random.default_rng(7)
     B, ticks = 96, 3
     prm = O.ForceParams()
     O.lib().qo_force_params_default(C.byref(prm))
+    if hw:
+        prm.mass, prm.mu = 14.0, 0.5
     states = []
     for b in range(B):
         s = O.DynState()
         O.lib().qo_dyn_init(C.byref(s))
         states.append(s)
-    solver = qp.ForceQP(batch=B, device=dev)
+    solver = qp.ForceQP(batch=B, device=dev, grouped=grouped, hw=hw)
+    assert (solver.params.mass, solver.params.mu) == ((14.0, 0.5) if hw else (12.0, 0.25))
     exact, total = 0, 0
     for tick in range(ticks):
         inp = force_inputs(rng, B)
@@ -211,6 +221,31 @@ def test_force_qp_grouped_launch_is_bit_identical():
                        np.where(m == 101, np.where(rs == 0, 3, np.where(rs == 1, 4, 0)), 0))
         key = pat * 16 + np.minimum(prev.cpu().numpy()[lst], 15)
         assert np.all(np.diff(key) >= 0), tick
+
+
+def test_hw_torque_ff_bit_exact():
+    """The hardware loop's feed-forward after force_opt (unitree_legged_real
+    torque_mode.cpp:1370-1384: stand-up ramp blend of grf_opt with the
+    stand-up GRF, tau = -J^T F, no gravity compensation) against the oracle's
+    restatement, bit for bit, over the ramp (dynamic_count 0 .. 700: rate 0,
+    partial, 1, clamped)."""
+    dev = _dev()
+    rng = np.random.default_rng(5)
+    B = 1003
+    J = rng.normal(0, 0.3, (B, 4, 9))
+    g = rng.normal(0, 40, (B, 12))
+    base = rng.normal(0, 30, (B, 12))
+    cnt = rng.integers(0, 700, B).astype(np.int32)
+    cnt[:4] = [0, 1, 500, 501]
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    tau = qp.hw_torque_ff(d(J), d(g), d(base), d(cnt)).cpu().numpy()
+    for b in range(B):
+        ref = np.zeros(12)
+        O.lib().qo_hw_torque_ff(O.P(np.ascontiguousarray(J[b])), O.P(g[b].copy()), O.P(base[b].copy()),
+                                int(cnt[b]), O.P(ref))
+        assert np.array_equal(tau[b], ref), (b, tau[b], ref)
+    with pytest.raises(ValueError):
+        qp.hw_torque_ff(d(J), d(g), d(base), d(cnt.astype(np.int64)))
 
 
 def test_body_mpc_matches_restatement_over_a_gait():

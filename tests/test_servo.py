@@ -78,3 +78,22 @@ def test_block_runs_qp_and_torques_over_ticks():
         assert np.all(o["qp_solution"] == 1) and np.all(np.isfinite(o["tau"]))
         # the force QP balances the desired wrench up to its regularisation
         assert np.all(o["grf_opt"][:, 2::3].sum(1) > 0)
+
+
+def test_hw_torque_ff_restatement():
+    """oracle qo_hw_torque_ff (unitree_legged_real torque_mode.cpp:1370-1384)
+    against an independent numpy restatement: rate = min((count / 500)^2, 1),
+    F_opt = rate (grf_opt - base) + base per leg, tau = -J' F_opt (J col-major
+    per leg, no gravity compensation)."""
+    rng = np.random.default_rng(2)
+    for count in (0, 1, 250, 499, 500, 501, 10000):
+        J = rng.normal(0, 0.3, (4, 9))
+        g, base = rng.normal(0, 40, 12), rng.normal(0, 30, 12)
+        tau = np.zeros(12)
+        O.lib().qo_hw_torque_ff(O.P(np.ascontiguousarray(J)), O.P(g.copy()), O.P(base.copy()), count,
+                                O.P(tau))
+        rate = min((count / 500.0) ** 2, 1.0)
+        for leg in range(4):
+            Jm = J[leg].reshape(3, 3).T  # col-major
+            F = rate * (g[3 * leg:3 * leg + 3] - base[3 * leg:3 * leg + 3]) + base[3 * leg:3 * leg + 3]
+            assert np.allclose(tau[3 * leg:3 * leg + 3], -(Jm.T @ F), rtol=1e-13, atol=1e-12), (count, leg)

@@ -9,8 +9,11 @@
 #   smoke        __graft_entry__.smoke()                 -> smoke.log
 #   bench        python bench.py (default line)          -> bench.json
 #   ktrace       rocprofv3 --kernel-trace --stats of the bench -> kernel_stats.csv
-#   sq[=VAR]     two SQ counter passes of perf_kernel.py VAR (default) -> pmc_sq.txt
-#   traffic[=VAR] FETCH_SIZE / WRITE_SIZE passes          -> traffic_*.json
+#   ktraceh      headline-only kernel trace (--no-second-line), last 50 launches -> kernel_stats_headline.csv
+#   sq[=VAR]     two SQ counter passes of perf_kernel.py VAR (default; env N, GAIT, LITERAL, TB = batch)
+#                                                         -> pmc_sq_n*_b*_lit*.txt
+#   sqqp[=ARGS]  two SQ counter passes of the grouped force-QP launch (tools/bench_qp.py) -> pmc_sq_qp.txt
+#   traffic[=VAR] FETCH_SIZE / WRITE_SIZE passes (env as sq) -> traffic_*.json
 #   configs      bench lines of configs 3-5 (per-GPU shares) -> configs.jsonl
 #   lit          literal-QP lines at N = 10 / 16 / 20     -> literal.jsonl
 #   breakdown    perf_kernel.py ablations (setup / iterations / checks), reduced + literal
@@ -57,24 +60,42 @@ for step in "$@"; do
         --no-cpu-baseline ${arg//:/ } > "$out/ktrace.log" 2>&1 || fail "$out/ktrace.log"
       python tools/db_kernel_stats.py "$out/ktrace" > "$out/kernel_stats.csv" && rm -rf "$out/ktrace"
       head -5 "$out/kernel_stats.csv" ;;
+    ktraceh)
+      # headline only (no side lines), stats over the K timed launches
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/ktraceh" -o run -- python bench.py --steps 50 --warmup 5 \
+        --no-second-line --no-cpu-baseline ${arg//:/ } > "$out/ktraceh.log" 2>&1 || fail "$out/ktraceh.log"
+      python tools/db_kernel_stats.py "$out/ktraceh" --last 50 > "$out/kernel_stats_headline.csv" && rm -rf "$out/ktraceh"
+      head -5 "$out/kernel_stats_headline.csv"; tail -1 "$out/ktraceh.log" ;;
     sq)
       v=${arg:-default}
       timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
-        SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d "$out/pmc1" -o run -- python tools/perf_kernel.py "$v" 4096 3 \
+        SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d "$out/pmc1" -o run -- python tools/perf_kernel.py "$v" ${TB:-4096} 3 \
         > "$out/pmc1.log" 2>&1 || fail "$out/pmc1.log"
       timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM \
-        SQ_INSTS_SALU GRBM_GUI_ACTIVE -d "$out/pmc2" -o run -- python tools/perf_kernel.py "$v" 4096 3 \
+        SQ_INSTS_SALU GRBM_GUI_ACTIVE -d "$out/pmc2" -o run -- python tools/perf_kernel.py "$v" ${TB:-4096} 3 \
         > "$out/pmc2.log" 2>&1 || fail "$out/pmc2.log"
-      python tools/pmc_summary.py "$out/pmc1" srbd > "$out/pmc_sq.txt" && python tools/pmc_summary.py "$out/pmc2" srbd >> "$out/pmc_sq.txt"
+      sqf="$out/pmc_sq_n${N:-10}_${GAIT:-trot}_b${TB:-4096}_lit${LITERAL:-0}.txt"
+      python tools/pmc_summary.py "$out/pmc1" srbd > "$sqf" && python tools/pmc_summary.py "$out/pmc2" srbd >> "$sqf"
       rm -rf "$out/pmc1" "$out/pmc2"
-      cat "$out/pmc_sq.txt" ;;
+      cat "$sqf" ;;
+    sqqp)
+      # SQ counters of the grouped force-QP launch (tools/bench_qp.py, 65,536 robots)
+      for p in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
+               "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM SQ_INSTS_SALU GRBM_GUI_ACTIVE"; do
+        n=$((n + 1))
+        timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $p -d "$out/pmcq$n" -o run -- python tools/bench_qp.py \
+          --steps 3 --warmup 2 --no-cpu-baseline ${arg//:/ } > "$out/pmcq$n.log" 2>&1 || fail "$out/pmcq$n.log"
+        python tools/pmc_summary.py "$out/pmcq$n" force_qp >> "$out/pmc_sq_qp.txt"
+        rm -rf "$out/pmcq$n"
+      done
+      cat "$out/pmc_sq_qp.txt" ;;
     traffic)
       v=${arg:-default}
-      timeout -s KILL 90 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$out/fetch" -o run -- python tools/perf_kernel.py "$v" 4096 3 \
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$out/fetch" -o run -- python tools/perf_kernel.py "$v" ${TB:-4096} 3 \
         > "$out/fetch.log" 2>&1 || fail "$out/fetch.log"
-      timeout -s KILL 90 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$out/write" -o run -- python tools/perf_kernel.py "$v" 4096 3 \
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$out/write" -o run -- python tools/perf_kernel.py "$v" ${TB:-4096} 3 \
         > "$out/write.log" 2>&1 || fail "$out/write.log"
-      python tools/prof_summary.py traffic "$out/fetch" "$out/write" srbd "$out/traffic_${v}_lit${LITERAL:-0}.json"
+      python tools/prof_summary.py traffic "$out/fetch" "$out/write" srbd "$out/traffic_${v}_n${N:-10}_${GAIT:-trot}_b${TB:-4096}_lit${LITERAL:-0}.json"
       rm -rf "$out/fetch" "$out/write" ;;
     configs)
       for spec in "16 trot 65536" "20 pace 65536" "10 mixed 131072"; do

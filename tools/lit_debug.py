@@ -19,10 +19,14 @@ gait = sys.argv[2] if len(sys.argv) > 2 else "trot"
 N = int(os.environ.get("N", 10))
 dev = torch.device("cuda:0")
 x0, xr, ft, ct = srbd.generate(20261015, N, B, gait)
+# QSET: one of srbd.REFERENCE_WEIGHTS (default: the Go1 weights)
+QSET = os.environ.get("QSET")
+Q_W, R_W = srbd.REFERENCE_WEIGHTS[QSET] if QSET else (O.Q_W, O.R_W)
+WKW = dict(q_weights=Q_W, r_weights=R_W) if QSET else {}
 
 
 def solve(idx, **kw):
-    s = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=1, **kw)
+    s = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=1, **WKW, **kw)
     args = [torch.from_numpy(np.ascontiguousarray(a[idx])).to(dev) for a in (x0, xr, ft, ct)]
     out = s.solve(*args, full=True)
     torch.cuda.synchronize()
@@ -30,7 +34,7 @@ def solve(idx, **kw):
 
 
 if len(sys.argv) > 3 and sys.argv[3] == "rho":
-    sp = O.srbd_spec(N=N)
+    sp = O.srbd_spec(N=N, q_w=Q_W, r_w=R_W)
     bl = [int(x) for x in os.environ.get("INST", "1454,2647,1").split(",")]
     for b in bl:
         inst = Instance(sp, x0[b], xr[b], ft[b], ct[b])
@@ -47,7 +51,7 @@ r = solve(np.arange(B))
 bad = np.nonzero(r["status"] != 0)[0]
 print("batch", B, gait, "status counts", np.unique(r["status"], return_counts=True), "iters mean",
       r["iters"].mean(), "max", r["iters"].max(), flush=True)
-sp = O.srbd_spec(N=N)
+sp = O.srbd_spec(N=N, q_w=Q_W, r_w=R_W)
 print("bad", bad[:40].tolist(), flush=True)
 for b in bad[:6]:
     alone = solve(np.array([b]))

@@ -26,7 +26,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 PATCH = ("qloco_srbd_lit.hip:    bool refactor = false;\n=>"
          "    bool refactor = false;\n"
-         "    if (a.warm && a.warm_start == 0 && rho_updates == 0) {\n"
+         "    if (a.warm && a.warm_start == 0 && S.sc[wv].rho_updates == 0) {\n"
          "      float *dst = a.warm + ((int64_t)b * (64 * W) + threadIdx.x) * (60 * W);\n"
          "#pragma unroll\n"
          "      for (int c = 0; c < 60 * W; ++c) dst[c] = T.k[c];\n"
@@ -50,8 +50,12 @@ def run(N, gait, idx, rhos):
     x0, xr, ft, ct = srbd.generate(20261015, N, idx + 1, gait)
     x0, xr, ft, ct = (np.ascontiguousarray(a[idx:idx + 1]) for a in (x0, xr, ft, ct))
     dev = torch.device("cuda:0")
-    inst = Instance(O.srbd_spec(N=N), x0[0], xr[0], ft[0], ct[0])
-    G, Vu = P.wrench_model(x0[0], ft[0], N)
+    # QSET: one of srbd.REFERENCE_WEIGHTS (default: the Go1 weights)
+    qs = os.environ.get("QSET")
+    q_w, r_w = srbd.REFERENCE_WEIGHTS[qs] if qs else (O.Q_W, O.R_W)
+    wkw = dict(q_weights=q_w, r_weights=r_w) if qs else {}
+    inst = Instance(O.srbd_spec(N=N, q_w=q_w, r_w=r_w), x0[0], xr[0], ft[0], ct[0])
+    G, Vu = P.wrench_model(x0[0], ft[0], N, q_w=q_w)
     Pm, q, A, D, E, c = P.ruiz(inst.H, inst.g, inst.A)
     l, u = inst.lb * E, inst.ub * E
     Rdiag = np.diag(inst.H - Vu.T @ G @ Vu)
@@ -62,7 +66,7 @@ def run(N, gait, idx, rhos):
         for ln in range(6 * nw):
             glob[(w, ln)] = 6 * (w * H + ln // 6) + ln % 6
     for rho in rhos:
-        s = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=1, rho=rho, adaptive_rho=0, max_iter=0)
+        s = srbd.BatchedConvexMpc(horizon=N, literal_full_qp=1, rho=rho, adaptive_rho=0, max_iter=0, **wkw)
         dump = torch.zeros((64 * W, 60 * W), dtype=torch.float32, device=dev)
         s.solve(*(torch.from_numpy(a).to(dev) for a in (x0, xr, ft, ct)), warm=dump)
         torch.cuda.synchronize()
