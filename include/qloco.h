@@ -155,18 +155,17 @@ int qloco_srbd_solve_ex(const qloco_srbd_spec *spec, int64_t batch, const float 
  * (host-only, no device work; the solve uses the same decision):
  *   QLOCO_ROUTE_LIT_ONE_WAVE  literal QP, N <= 10: srbd_lit_kernel (one wavefront
  *                             per instance, the OSQP solve through the wrench space)
- *   QLOCO_ROUTE_LIT_TWO_WAVE  literal QP, N = 11..20, state weights <= 1000:
- *                             srbd_lit2_kernel
+ *   QLOCO_ROUTE_LIT_TWO_WAVE  literal QP, N = 11..20: srbd_lit2_kernel
  *   QLOCO_ROUTE_LIT_GENERIC   literal QP otherwise (a q_omega / q_v weight of 0,
- *                             per-step feet, N > 20, or N > 10 with a state
- *                             weight above 1000): the 12N-variable kernels
+ *                             a state weight above 1000, per-step feet, N > 20):
+ *                             the 12N-variable kernels
  *   QLOCO_ROUTE_REDUCED       literal_full_qp = 0: the stance-only classes
- * At N <= 10 any q_weights with q_omega, q_v > 0 -- the Go1 defaults and all
- * three of the reference's config/{gazebo,hardware,isaac}_a1_mpc.yaml sets,
- * isaac's anisotropic omega weights included -- take the one-wave
- * wrench-space kernel; at N = 11..20 the Go1 / gazebo / hardware sets take
- * the two-wave one and isaac's (roll 8000) the generic kernels (the two-wave
- * kernel's float32 solve).  Returns QLOCO_ERR_ARG on a bad spec. */
+ * The Go1 defaults and the reference's config/{gazebo,hardware}_a1_mpc.yaml
+ * sets take the wrench-space kernels, and so would anisotropic omega
+ * weights of that size; config/isaac_a1_mpc.yaml's (roll 8000) take the
+ * generic ones, where float32 converges as float64 does (the wrench-space
+ * solve's precision limit).  Returns QLOCO_ERR_ARG on a bad
+ * spec. */
 #define QLOCO_ROUTE_LIT_ONE_WAVE 1
 #define QLOCO_ROUTE_LIT_TWO_WAVE 2
 #define QLOCO_ROUTE_LIT_GENERIC 3

@@ -1488,30 +1488,29 @@ extern "C" int qloco_srbd_max_stance_vars(void) { return 3 * kBigLegs; }
 
 // Which kernel family a call takes (qloco_srbd_route).  The wrench-space
 // kernels build G^-1 from per-axis blocks: that needs every
-// q_omega and q_v > 0 (G positive definite; any q_theta / q_p >= 0, the
-// omega x / y block is one 2N x 2N float64 Gauss-Jordan, so anisotropic
-// omega weights such as isaac_a1_mpc.yaml's stay on them) and feet constant
-// over the horizon (the wrench map Bb is per instance).  The two-wave kernel
-// (N = 11..20) also needs state weights of at most kLit2MaxQ: its float32
-// push-through solve x = a - W0^-1 Vu' T Vu a cancels more digits as the
-// wrench part of P grows against R at small rho, and with isaac's weights
-// (roll 8000, z 6020, v 2130) 6-19 % of N = 11..16 instances stop converging
-// at rho <= 3e-4 where float64 converges -- T rounded from an exact float64
-// inverse does the same in emulation, so it is the form's precision, not
-// the Gauss-Jordan's (tools/lit_weights_numerics.py); the Go1
-// / gazebo / hardware sets (<= 420) match the float64 iteration counts.
-// Other literal calls take the generic literal kernels.
-constexpr float kLit2MaxQ = 1000.0f;
+// q_omega and q_v > 0 (G positive definite; any q_theta / q_p >= 0 -- the
+// omega x / y pair is diagonalised with the yaw-rotated q_theta, so
+// anisotropic omega weights stay on them) and feet constant over the
+// horizon (the wrench map Bb is per instance).  They also need state
+// weights of at most kLitMaxQ: their float32 push-through solve
+// x = a - W0^-1 Vu' T Vu a cancels more digits as the wrench part of P grows
+// against R at small rho, and with isaac_a1_mpc.yaml's weights (roll 8000,
+// z 6020, v 2130) 1-2 % of N = 10 and 6-19 % of N = 11..16 instances stop
+// converging at rho <= 3e-4 where float64 converges; T rounded from an exact
+// float64 inverse does the same in emulation, so it is the form's precision,
+// not the Gauss-Jordan's (tools/lit_weights_numerics.py).  The
+// Go1 / gazebo / hardware sets (<= 420) match the float64 iteration counts.
+// Other literal calls take the generic literal kernels (the 12N-variable
+// KKT inverse), which converge on isaac's weights as float64 does.
+constexpr float kLitMaxQ = 1000.0f;
 static int srbd_route_of(const SrbdArgs &a) {
   if (!a.literal) return QLOCO_ROUTE_REDUCED;
   const bool lit_blocks = a.q2[6] > 0.0f && a.q2[7] > 0.0f && a.q2[8] > 0.0f && a.q2[9] > 0.0f &&
                           a.q2[10] > 0.0f && a.q2[11] > 0.0f;
   float qmax = 0.0f;
   for (int k = 0; k < 12; ++k) qmax = fmaxf(qmax, 0.5f * a.q2[k]);
-  if (a.N <= kLitN2 && !a.feet_per_step && lit_blocks) {
-    if (a.N <= kLitN) return QLOCO_ROUTE_LIT_ONE_WAVE;
-    if (qmax <= kLit2MaxQ) return QLOCO_ROUTE_LIT_TWO_WAVE;
-  }
+  if (a.N <= kLitN2 && !a.feet_per_step && lit_blocks && qmax <= kLitMaxQ)
+    return a.N <= kLitN ? QLOCO_ROUTE_LIT_ONE_WAVE : QLOCO_ROUTE_LIT_TWO_WAVE;
   return QLOCO_ROUTE_LIT_GENERIC;
 }
 

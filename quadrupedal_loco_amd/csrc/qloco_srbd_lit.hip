@@ -78,33 +78,22 @@ struct LitLds {
   // it across the ADMM iterations
   struct {
     float rho, cs, cinv, qn0, qn1, alpha, oma, sigma, dtm;
+    float sxy[2][2];  // S of the omega x / y block: G^-1 = sum_a S[.][a] A_a^-1 S[.][a] (see the G^-1 tables)
     int iter, status, rho_updates, ctm, interval;
   } sc[W];
-  // G^-1 in world-frame blocks per (row step j, column step
-  // k), column-space steps: xy[a][b] = G^-1[(j, omega_a), (k, omega_b)] (a, b
-  // in {x, y}: the omega x / y axes couple when q_omega_x != q_omega_y) and
-  // zv = (omega_z, v_x, v_y, v_z) diagonal blocks.  G^-1 is symmetric, so only
-  // j <= k is stored (entry k (k + 1) / 2 + j; block (k, j) is the transpose
-  // of block (j, k)).  Written once per solve (the pivot-row exchange of its
-  // float64 Gauss-Jordans runs in this area before), read by every
-  // factorisation.
-  struct alignas(16) GInv {
-    f4v xy;  // (xx, xy, yx, yy)
-    f4v zv;
-  } gtab[NT * (NT + 1) / 2];
   union alignas(16) {       // phase-local storage (LDS bounds the one-wave occupancy: <= 10 KB;
                             // 16-byte aligned: dcol is read as f4v, a misaligned ds_read_b128
                             // cost the one-wave kernel 46 us per launch)
-    struct {                // gradient
+    struct {                // gradient + Ruiz
+      f2v beps[12][12];     // (beta, eps)[w][w']: the P entries' per-column coefficients
+      float dcol[12 * NT];  // Ruiz column scales D (read as same-address broadcasts)
       float err[12 * NT];   // gradient scans
       float Wc[12 * NT];
     };
-    struct {                // Ruiz
-      f2v beps[12][12];     // (beta, eps)[w][w']: the P entries' per-column coefficients
-      float dcol[12 * NT];  // Ruiz column scales D (read as same-address broadcasts)
-    };
     struct {                // factorisation
       float w0i[W][3][2][64];   // per variable its row of W0^-1 (x, y, z), read by the U rows
+      f2v gtab[NT][NT][3];      // G^-1 blocks: per (row step, column step) in
+                                // column-space order, (W0, W1), (W2, V0), (V1, V2)
     };
   };
   float piv[W == 1 ? 0 : 2];       // two waves: the Gauss-Jordan pivot, [parity]
@@ -914,115 +903,122 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
       }
     }
   }
-  // G^-1 in world-frame blocks.  G = K0 (x) Qb + K2 (x) Te
+  // G^-1 in six N x N blocks.  G = K0 (x) Qb + K2 (x) Te
   // (Qb = diag(q_omega, q_v), Te = dt^2 blockdiag(Rz' diag(q_theta) Rz,
   // diag(q_p))) splits by wrench component: each v axis and omega_z alone
-  // (A_a = alpha_a K0 + beta_a K2, N x N), omega_x / omega_y together
-  // (G_xy = K0 (x) diag(q_omega_x, q_omega_y) + K2 (x) dt^2 [Rz' Q_theta Rz]_xy,
-  // 2N x 2N: the two axes couple through the yaw rotation unless
-  // q_omega_x == q_omega_y, which the Go1 weights have and the reference's
-  // isaac_a1_mpc.yaml does not).  Each row of the five blocks is one lane's
-  // float64 Gauss-Jordan row, once per solve, instead of a 6N x 6N one per
-  // factorisation.  Lanes: r < 2N the xy block (axis a = r / N, step r % N;
-  // columns b N + k), then omega_z, v_x, v_y, v_z (N rows each).
+  // (A_a = alpha_a K0 + beta_a K2), omega_x / omega_y together:
+  // G_xy = K0 (x) Q + K2 (x) dt^2 T, Q = diag(q_omega_x, q_omega_y),
+  // T = [Rz' diag(q_theta) Rz]_xy.  The 2 x 2 pair (T, Q) is diagonalised
+  // together -- S' Q S = I, S' T S = diag(lambda) with S = Q^-1/2 V, V the
+  // eigenvectors of Q^-1/2 T Q^-1/2 (one Jacobi rotation) -- so
+  // G_xy^-1 = (I (x) S) diag_a (K0 + dt^2 lambda_a K2)^-1 (I (x) S'): two more
+  // N x N inverses, recombined through S in the factorisation.  Any omega
+  // weights work (q_omega_x != q_omega_y couples the axes: the reference's
+  // isaac_a1_mpc.yaml); with q_omega_x = q_omega_y S is Rz' / sqrt(q_omega).
+  // One N x N Gauss-Jordan per (axis, row) lane in float64, once per solve,
+  // instead of a 6N x 6N one per factorisation.
   float gmx;  // max diag G^-1 (block-uniform; an SPD matrix's largest entry)
   {
-    constexpr int NC = 2 * NS;  // register row: the xy block's 2N columns (the N x N blocks use NS)
-    double row[NC];
+    double row[NS];
     const int r = tid;
     const bool live = r < 6 * N;
-    const bool bxy = r < 2 * N;
-    // block (0: xy, 1: omega_z, 2..4: v), axis within xy, step of the row
-    const int blk = !live ? 0 : (bxy ? 0 : 1 + (r - 2 * N) / N);
-    const int axy = bxy ? (r >= N ? 1 : 0) : 0;
-    const int ri = !live ? 0 : (bxy ? r - N * axy : (r - 2 * N) - N * ((r - 2 * N) / N));
-    const int own = bxy ? axy * NS + ri : ri;  // the row's own (diagonal) register column
+    const int ax = live ? r / N : 0, ri = live ? r - N * (r / N) : 0;
+    double sxy[2][2], sn2 = 1.0;  // S; sn2: this lane's axis' S column norm^2 (the gmx bound)
     {
       const double dt2 = (double)dt * (double)dt;
-      // world-frame 2 x 2 coefficients of the row's axis against column axis b
-      double al[2], be[2];
+      double lam[2];
       {
+        const double qx = (double)S.q2[6], qy = (double)S.q2[7];
         const double yw = (double)S.x0[2], cw = cos(yw), sw = sin(yw);
         const double Rm[2][2] = {{cw, sw}, {-sw, cw}};  // Rz (A1RobotControl.cpp:506-508)
+        double T[2][2];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          // [Rz' diag(q_theta) Rz]_(a, b) = sum_m Rz[m][a] q_theta_m Rz[m][b]
-          const double tq = Rm[0][axy] * (double)S.q2[0] * Rm[0][b] + Rm[1][axy] * (double)S.q2[1] * Rm[1][b];
-          al[b] = b == axy ? (double)S.q2[6 + axy] : 0.0;
-          be[b] = dt2 * tq;
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            T[i][j] = Rm[0][i] * (double)S.q2[0] * Rm[0][j] + Rm[1][i] * (double)S.q2[1] * Rm[1][j];
+        const double ix = 1.0 / sqrt(qx), iy = 1.0 / sqrt(qy);
+        const double c00 = T[0][0] * ix * ix, c01 = T[0][1] * ix * iy, c11 = T[1][1] * iy * iy;
+        double t = 0.0;  // one Jacobi rotation: tan of the angle that diagonalises C
+        if (c01 != 0.0) {
+          const double tau = (c11 - c00) / (2.0 * c01);
+          t = tau == 0.0 ? 1.0 : (tau > 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
         }
-        if (!bxy) {  // omega_z: q2[8] / q2[2]; v axes: q2[9..11] / q_p q2[3..5]
-          const int ax = blk + 1;  // 2 .. 5
-          al[0] = ax == 2 ? (double)S.q2[8] : (double)S.q2[9 + ax - 3];
-          be[0] = dt2 * (double)S.q2[ax];
-          al[1] = be[1] = 0.0;
-        }
+        const double cs = 1.0 / sqrt(1.0 + t * t), sn = t * cs;
+        lam[0] = c00 - t * c01;
+        lam[1] = c11 + t * c01;
+        sxy[0][0] = ix * cs;  // S = Q^-1/2 V, V = [[cs, sn], [-sn, cs]]
+        sxy[0][1] = ix * sn;
+        sxy[1][0] = -iy * sn;
+        sxy[1][1] = iy * cs;
+        if (ax < 2) sn2 = sxy[0][ax] * sxy[0][ax] + sxy[1][ax] * sxy[1][ax];
       }
+      const double al = ax < 2 ? 1.0 : (ax == 2 ? (double)S.q2[8] : (double)S.q2[9 + ax - 3]);
+      const double be = ax < 2 ? dt2 * lam[ax] : dt2 * (double)S.q2[ax];  // q_theta_z / q_p: q2[2..5]
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int b = c >= NS ? 1 : 0, k = c - NS * b;
+      for (int k = 0; k < NS; ++k) {
         const int M = ri > k ? ri : k;
         const double T0 = (double)(N - M), ia = (double)(M - ri), ib = (double)(M - k);
         const double S1 = 0.5 * T0 * (T0 - 1.0), S2 = (T0 - 1.0) * T0 * (2.0 * T0 - 1.0) / 6.0;
         const double K2 = S2 + (ia + ib) * S1 + ia * ib * T0;
-        const bool in = live && k < N && (b == 0 || bxy);
-        row[c] = in ? fma(al[b], T0, be[b] * K2) : 0.0;
+        row[k] = (live && k < N) ? fma(al, T0, be * K2) : (k == ri ? 1.0 : 0.0);
       }
     }
-    // register column c of a row <-> block column: c < NS: (b = 0, k = c),
-    // else (b = 1, k = c - NS); pivots in register-column order (xy: 2N
-    // pivots, the single-axis blocks N)
     // in-place Gauss-Jordan, the pivot row through LDS (double-buffered in the
     // table area, which is written only after the last pivot)
-    double *xch = reinterpret_cast<double *>(&S.gtab[0]);
-    static_assert(sizeof(S.gtab) >= 2 * 5 * NC * sizeof(double), "pivot-row exchange fits the table area");
+    double *xch = reinterpret_cast<double *>(&S.gtab[0][0][0]);
+    static_assert(sizeof(S.gtab) >= 2 * 6 * NS * sizeof(double), "pivot-row exchange fits the table area");
 #pragma unroll
-    for (int kk = 0; kk < NC; ++kk) {
-      const int pb = kk >= NS ? 1 : 0, pk = kk - NS * pb;  // pivot: block column (pb, pk)
-      if (pk >= N) continue;  // uniform; not a break (the loop must unroll: row[] stays in registers)
-      double *buf = xch + (kk & 1) * (5 * NC);
-      const bool mine = live && (pb == 0 || bxy);  // this row's block has this pivot
-      if (mine && own == kk) {
+    for (int k = 0; k < NS; ++k) {
+      if (k >= N) continue;  // uniform; not a break (the loop must unroll: row[] stays in registers)
+      double *buf = xch + (k & 1) * (6 * NS);
+      if (live && ri == k) {
 #pragma unroll
-        for (int c = 0; c < NC; ++c) buf[blk * NC + c] = row[c];
+        for (int c = 0; c < NS; ++c) buf[ax * NS + c] = row[c];
       }
       bsync<W>();
-      if (mine) {
-        const double *pr = buf + blk * NC;  // the pivot row, read as it is used (no second register row)
-        const double pinv = 1.0 / pr[kk];
-        const double fk = row[kk] * pinv;
-        const bool piv = own == kk;
+      const double *pr = buf + ax * NS;  // the pivot row, read as it is used (no second register row)
+      const double pinv = 1.0 / pr[k];
+      const double fk = row[k] * pinv;
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          if (c == kk) continue;
-          const double pc = pr[c];
-          row[c] = piv ? pc * pinv : fma(-fk, pc, row[c]);
-        }
-        row[kk] = piv ? pinv : -fk;
+      for (int c = 0; c < NS; ++c) {
+        if (c == k) continue;
+        const double pc = pr[c];
+        row[c] = ri == k ? pc * pinv : fma(-fk, pc, row[c]);
       }
+      row[k] = ri == k ? pinv : -fk;
     }
     bsync<W>();
     // the padding entries of the tables are zero
-    for (int idx = tid; idx < NT * (NT + 1) / 2 * 8; idx += 64 * W) reinterpret_cast<float *>(&S.gtab[0])[idx] = 0.0f;
+    for (int idx = tid; idx < NT * NT * 3; idx += 64 * W) (&S.gtab[0][0][0])[idx] = (f2v)(0.0f);
     bsync<W>();
     float dmax = 0.0f;
     if (live) {
       const int csi = W == 1 ? ri : (ri < H ? ri : 10 + ri - H);
+      float *dst = reinterpret_cast<float *>(&S.gtab[csi][0][0]);
 #pragma unroll
       for (int k = 0; k < NS; ++k) {
-        const int csk = W == 1 ? k : (k < H ? k : 10 + k - H);
-        if (k < N && csi <= csk) {  // the stored triangle
-          float *e = reinterpret_cast<float *>(&S.gtab[csk * (csk + 1) / 2 + csi]);
-          if (bxy) {
-            e[2 * axy] = (float)row[k];           // (a, x)
-            e[2 * axy + 1] = (float)row[NS + k];  // (a, y)
-          } else {
-            e[4 + blk - 1] = (float)row[k];
-          }
+        if (k < N) {
+          const int csk = W == 1 ? k : (k < H ? k : 10 + k - H);
+          dst[csk * 6 + ax] = (float)row[k];
         }
+        // world-frame diagonal of the xy block <= 2 max_a |S[.][a]|^2 A_a^-1(j, j)
+        dmax = k == ri ? (float)(sn2 * row[k]) : dmax;
       }
+    }
+    if (tid == 0) {
 #pragma unroll
-      for (int c = 0; c < NC; ++c) dmax = c == own ? (float)row[c] : dmax;
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) S.sc[wv].sxy[i][j] = (float)sxy[i][j];
+    }
+    if constexpr (W == 2) {
+      if (tid == 64) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) S.sc[1].sxy[i][j] = (float)sxy[i][j];
+      }
     }
     gmx = sgpr_f(bmax1<W>(S, wmax_nonneg(dmax), wv));
     bsync<W>();
@@ -1115,8 +1111,8 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
         }
       }
       // T = (I + cG U)^-1 cG = (U + (cG)^-1)^-1: this lane's
-      // row of M = G^-1 / c + U (G^-1 from the per-solve world-frame tables;
-      // U block-diagonal: this lane's row of U_jr in
+      // row of M = G^-1 / c + U (G^-1 from the per-solve tables through the
+      // omega block's rotation; U block-diagonal: this lane's row of U_jr in
       // its own step's six columns), scaled by 1 / (max diag G^-1 / c + max
       // diag U) -- a bound within 2x of max diag M (SPD) -- and inverted in
       // place.  (Round 4's S = I + L'cGL form left a KKT backward error of
@@ -1128,23 +1124,23 @@ __device__ __forceinline__ void srbd_lit_one(const SrbdArgs &a, LitLds<W> &S, co
 #pragma unroll
         for (int t = 0; t < 6; ++t) uii = t == sr ? Urow[t] : uii;
         sM = sgpr_f(1.0f / fmaf(gmx, cinv, bmax1<W>(S, wmax_nonneg(wvalid ? uii : 0.0f), wv)));
-        // this row's entries of the world-frame G^-1 blocks: omega x / y rows
-        // their xy pair, the other rows their own axis's diagonal block
-        const float m0 = sr == 0 ? 1.0f : 0.0f, m1 = sr == 1 ? 1.0f : 0.0f, m2 = sr == 2 ? 1.0f : 0.0f,
-                    m3 = sr == 3 ? 1.0f : 0.0f, m4 = sr == 4 ? 1.0f : 0.0f, m5 = sr == 5 ? 1.0f : 0.0f;
+        // omega x / y block coefficients S[sr][a] S[t][a], a, t in {0, 1}
+        // (the G^-1 tables hold the eigen axes' A_a^-1)
+        const float s00 = uf(S.sc[wv].sxy[0][0]), s01 = uf(S.sc[wv].sxy[0][1]), s10 = uf(S.sc[wv].sxy[1][0]),
+                    s11 = uf(S.sc[wv].sxy[1][1]);
+        const float r0 = sr == 0 ? s00 : (sr == 1 ? s10 : 0.0f), r1 = sr == 0 ? s01 : (sr == 1 ? s11 : 0.0f);
+        const float c00 = r0 * s00, c01 = r0 * s10, c10 = r1 * s01, c11 = r1 * s11;
+        const float m2 = sr == 2 ? 1.0f : 0.0f, m3 = sr == 3 ? 1.0f : 0.0f, m4 = sr == 4 ? 1.0f : 0.0f,
+                    m5 = sr == 5 ? 1.0f : 0.0f;
         const float scale = sM * cinv;
 #pragma unroll
         for (int wp = 0; wp < W; ++wp) {
 #pragma unroll
           for (int k = 0; k < kLitN; ++k) {
-            // block (jc, kc) of the symmetric table: stored as (kc, jc) transposed when jc > kc
-            const int kc = 10 * wp + k;
-            const bool up = jc <= kc;
-            const auto &ge = S.gtab[up ? kc * (kc + 1) / 2 + jc : jc * (jc + 1) / 2 + kc];
-            const f4v exy = ge.xy, ezv = ge.zv;
-            const float exy1 = up ? exy.y : exy.z, exy2 = up ? exy.z : exy.y;  // (x, y) / (y, x)
-            const float gv[6] = {fmaf(m0, exy.x, m1 * exy2), fmaf(m0, exy1, m1 * exy.w), m2 * ezv.x,
-                                 m3 * ezv.y, m4 * ezv.z, m5 * ezv.w};
+            const f2v e0 = S.gtab[jc][10 * wp + k][0], e1 = S.gtab[jc][10 * wp + k][1],
+                      e2 = S.gtab[jc][10 * wp + k][2];
+            const float gv[6] = {fmaf(c00, e0.x, c10 * e0.y), fmaf(c01, e0.x, c11 * e0.y), m2 * e1.x,
+                                 m3 * e1.y, m4 * e2.x, m5 * e2.y};
             const bool blk = wp == wv && k == jr;  // this row's own step block
 #pragma unroll
             for (int t = 0; t < 6; ++t) {

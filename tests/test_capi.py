@@ -76,19 +76,24 @@ def test_force_params_defaults():
 @pytest.mark.parametrize("weights", ["default", "gazebo", "hardware", "isaac"])
 def test_srbd_route_keeps_reference_weights_on_the_wrench_space_kernels(weights):
     """qloco_srbd_route (host-only): the literal QP with the Go1 defaults and
-    with every weight set the reference ships (config/*_a1_mpc.yaml, isaac's
-    anisotropic omega weights included) runs the one-wave wrench-space
-    kernel at N <= 10; at 11..20 the two-wave one, except isaac's (state
-    weights above 1000: the generic kernels); a zero omega / v
-    weight or per-step feet take the generic literal kernels;
-    literal_full_qp = 0 the reduced classes."""
+    the reference's gazebo / hardware weight sets runs the wrench-space
+    kernels -- one wave at N <= 10, two at 11..20; isaac's (state weights
+    above 1000: the wrench-space solve's float32 limit), a
+    zero omega / v weight or per-step feet take the generic literal kernels;
+    literal_full_qp = 0 the reduced classes; an anisotropic omega weight of
+    moderate size stays on the wrench-space kernels."""
     kw = {} if weights == "default" else dict(zip(("q_weights", "r_weights"), srbd.REFERENCE_WEIGHTS[weights]))
-    two = 3 if weights == "isaac" else 2  # isaac's state weights exceed the two-wave kernel's 1000
-    for N, want in ((1, 1), (10, 1), (11, two), (16, two), (20, two)):
+    stiff = weights == "isaac"  # state weights above the wrench-space kernels' 1000
+    for N, want in ((1, 1), (10, 1), (11, 2), (16, 2), (20, 2)):
+        want = 3 if stiff else want
         assert srbd.route(srbd.default_spec(horizon=N, literal_full_qp=1, **kw)) == want, (N, weights)
     assert srbd.route(srbd.default_spec(horizon=10, literal_full_qp=0, **kw)) == 4
     assert srbd.route(srbd.default_spec(horizon=10, literal_full_qp=1, feet_per_step=1, **kw)) == 3
     q = list(srbd.default_spec(**kw).q_weights)
+    if not stiff:
+        q2 = list(q)
+        q2[7] = 2.0 * q2[6] + 0.3  # anisotropic omega weights
+        assert srbd.route(srbd.default_spec(horizon=16, literal_full_qp=1, q_weights=q2)) == 2
     q[9] = 0.0
     assert srbd.route(srbd.default_spec(horizon=10, literal_full_qp=1, q_weights=q)) == 3
     bad = srbd.default_spec(horizon=0)

@@ -174,13 +174,16 @@ def test_solve_refuses_bad_tensors_before_the_c_call():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [mgpu.CONTIGUOUS, mgpu.INTERLEAVED])
-@pytest.mark.parametrize("total,world,width", [(13, 3, 12), (13, 3, 14), (4099, 8, 14), (16, 4, 12)])
+@pytest.mark.parametrize("total,world,width", [(13, 3, 12), (13, 3, 14), (4099, 8, 14), (16, 4, 12),
+                                               (1048576, 8, 14), (1048573, 8, 14)])
 def test_device_reorder_matches_gather_rows(total, world, width, mode):
     """the device reorder of qloco_mgpu_solve (mgpu_unpack_kernel,
     padded shards, interleaved owners, the width-14 stats rows) had only run
     at world 1, where it is skipped.  qloco_mgpu_reorder runs it on one GPU on
     a synthetic gathered buffer for world > 1: every global id's row must land
-    where qloco_mgpu_gather_rows says, bit for bit, padding rows never read."""
+    where qloco_mgpu_gather_rows says, bit for bit, padding rows never read --
+    up to BASELINE configs[4]'s whole batch (1,048,576 at world 8, and one
+    short of it: padded shards)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     dev = torch.device("cuda:0")

