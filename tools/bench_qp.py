@@ -90,6 +90,11 @@ def main():
     ap.add_argument("--order", choices=("given", "pattern", "iters"), default="given",
                     help="experiment: permute the robots on the host before timing -- grouped by "
                          "swing-leg pattern, or by pattern then by a first solve's iteration count")
+    ap.add_argument("--ticks", type=int, default=1,
+                    help="distinct input sets cycled over the steps (tests/cases.force_inputs, one rng "
+                         "stream): with 1 every step re-solves the same inputs, so the grouping key (the "
+                         "previous call's iteration count) predicts the next call exactly -- the best "
+                         "case; with > 1 every call gets new inputs, as a servo tick does")
     ap.add_argument("--ungrouped", action="store_true",
                     help="the plain launch (qloco_force_qp_solve) instead of the grouped one")
     ap.add_argument("--servo", action="store_true",
@@ -117,16 +122,20 @@ def main():
             key = key + it0
         perm = np.argsort(key, kind="stable")
         inp = {k: v[perm] for k, v in inp.items()}
-    d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in inp.items()}
+    sets = [{k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in inp.items()}]
+    rng_t = np.random.default_rng(4)
+    for _ in range(args.ticks - 1):
+        sets.append({k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+                     for k, v in force_inputs(rng_t, B).items()})
     solver = qp.ForceQP(batch=B, device=dev, grouped=not args.ungrouped)
-    for _ in range(args.warmup):
-        out = solver.step(**d)
+    for k in range(args.warmup):
+        out = solver.step(**sets[k % len(sets)])
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     ev[0].record(stream)
     for k in range(args.steps):
-        out = solver.step(**d)
+        out = solver.step(**sets[(args.warmup + k) % len(sets)])
         ev[k + 1].record(stream)
     torch.cuda.synchronize()
     per = np.array([ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)])
@@ -141,9 +150,11 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms,
             "p99_batch_us": float(np.percentile(per, 99) * 1e3), "higher_is_better": True,
             "dtype": "f64", "data": "synthetic (tests/cases.force_inputs, seed 3)",
-            "config": {"workload": "force QP, %d robots, modes 101/102/103, right_support 0/1/2%s%s" % (
+            "config": {"workload": "force QP, %d robots, modes 101/102/103, right_support 0/1/2%s%s%s" % (
                 B, "" if args.order == "given" else ", host order: " + args.order,
-                ", ungrouped launch" if args.ungrouped else ", grouped launch (pattern, previous iterations)")},
+                ", ungrouped launch" if args.ungrouped else ", grouped launch (pattern, previous iterations)",
+                ", the same inputs every step" if args.ticks == 1 else
+                ", %d distinct input sets cycled (new inputs every step)" % args.ticks)},
             "gi_iters_mean": float(iters.mean()), "status_ok_frac": float(np.mean(status == 0)),
             "roofline": {"bound": "valu-fp64", "achieved": achieved, "peak": PEAK_FP64_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_FP64_TFLOPS,
