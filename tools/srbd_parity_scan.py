@@ -87,6 +87,8 @@ def main(cases, literal=False):
                 print("  du0 %-11s n %5d  p50 %9.4g p95 %9.4g p99 %9.4g max %9.4g  <=0.5N %.4f  <=2N %.4f" % (
                     nm, v.size, *np.percentile(v, [50, 95, 99]), v.max(), np.mean(v <= 0.5),
                     np.mean(v <= 2.0)))
+                print("  wrench %-11s max dF %9.4g N  max dM %9.4g N m  max dX_Q %9.4g" % (
+                    nm, R[sel, 1].max(), R[sel, 2].max(), R[sel, 3].max()))
         sys.stdout.flush()
 
 
