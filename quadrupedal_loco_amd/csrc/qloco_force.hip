@@ -10,6 +10,7 @@
 // skew_hat comma-operator bug (:379-381) and the F_prev = grf_opt coupling
 // (:305) are reproduced; a NaN solution falls back to F_leg_guess (:364-367).
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -54,18 +55,18 @@ __constant__ double c_force_CE[5][144];
 
 // Per group: A (6x12) is built in the solver's J and G in its R (both are
 // free until the solve starts, and the solver reads only G's lower triangle,
-// copying it in place), so a 4-robot block needs ~18 KB of LDS: 8 blocks per
-// CU, 2 waves per SIMD.
-// Per 4-robot block: each group's g0 and Goldfarb-Idnani work space (the
-// solution is read from gi.x).  The inequality rows are generated
-// (ForceCi), F_leg_guess stays in the owning lane's registers and ce0 is the
-// constant zero vector, so the block stays under 13.3 KB: 12 blocks -- three
-// waves -- per SIMD's share of a CU.
+// copying it in place); g0 lives in the solver's z (first written by
+// update_z in the equality loop, after the last reads of g0: the x0 solve and
+// f = g0'x / 2); the inequality rows are generated (ForceCi), F_leg_guess
+// stays in the owning lanes' registers, ce0 is the constant zero vector and
+// the solution is read from gi.x.  With byte-sized constraint indices a
+// group needs 3.36 KB: an 8-robot block (8-lane groups) 26.9 KB, six blocks
+// per CU; a 4-robot block (16-lane groups) 13.4 KB.
+template <int FG>
 struct ForceLds {
   struct Grp {
-    double g0[12];
     GiLdsT<12, 24, 12> gi;
-  } g[GI_GROUPS];
+  } g[FG];
 };
 
 __constant__ double c_force_zeros[16];
@@ -228,16 +229,19 @@ __device__ __forceinline__ void force_distribution(const double *com_des, const 
 // launch against 58 MB of algorithmic traffic (profiles/r3ft_traffic_force_
 // qp_b65536_wpe3.json) -- so the spill-free budget is the shipped one.
 constexpr int kForceWpe = 2;
+template <int GW>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kForceWpe))) void force_qp_kernel(
     const ForceArgs a) {
-  __shared__ ForceLds S;
-  const int lane = threadIdx.x, grp = lane >> 4, li = lane & 15;
-  const int64_t pos = (int64_t)blockIdx.x * GI_GROUPS + grp;
+  constexpr int FG = 64 / GW, VL = (12 + GW - 1) / GW;
+  __shared__ ForceLds<FG> S;
+  const int lane = threadIdx.x, grp = lane / GW, li = lane % GW;
+  const int64_t pos = (int64_t)blockIdx.x * FG + grp;
   if (pos >= a.batch) return;
   const int64_t inst = a.list ? a.list[pos] : pos;
-  ForceLds::Grp &P = S.g[grp];
+  typename ForceLds<FG>::Grp &P = S.g[grp];
   double *const PA = P.gi.J;  // A, 6x12 col-major (dead before J is formed)
   double *const PG = P.gi.R;  // G, 12x12 col-major (the solver's LLT workspace)
+  double *const Pg0 = P.gi.z;  // g0 (dead before z is first written)
 
   // ---- force_distribution (state F_leg_ref in/out) -> F_leg_guess
   double Fref[12];
@@ -245,14 +249,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kForceWpe)))
   force_distribution(a.com_des + inst * 3, a.leg_des + inst * 12, a.F_force_des + inst * 6,
                      a.mode[inst], a.y_coef[inst], a.rfoot_des + inst * 3, a.lfoot_des + inst * 3,
                      Fref);
-  // this lane's entry by a static select chain: indexing Fref by li would put
+  // this lane's entries by a static select chain: indexing Fref by li would put
   // the array in scratch (a per-lane spill of 96 B, written back to HBM)
-  double guess = Fref[0];  // F_leg_guess entry li (only lane li reads it)
+  double guess[VL];  // F_leg_guess entries li + GW v (only their lane reads them)
 #pragma unroll
-  for (int k = 1; k < 12; ++k) guess = (li == k) ? Fref[k] : guess;
+  for (int v = 0; v < VL; ++v) {
+    guess[v] = Fref[0];
+#pragma unroll
+    for (int k = 1; k < 12; ++k) guess[v] = (li + GW * v == k) ? Fref[k] : guess[v];
+  }
   // ---- force_opt: A (6x12, col-major) with the skew_hat quirk (:274-298)
-  if (li < 12) {
-    for (int k = 0; k < 6; ++k) PA[li * 6 + k] = 0.0;
+#pragma unroll
+  for (int v = 0; v < VL; ++v) {
+    const int r = li + GW * v;
+    if (r < 12)
+      for (int k = 0; k < 6; ++k) PA[r * 6 + k] = 0.0;
   }
   GI_SYNC();
   if (li < 4) {
@@ -271,38 +282,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kForceWpe)))
   // A'A(r,c) and A'A(c,r) are the same products summed in the same order, so G
   // is exactly symmetric and (G' + G)/2 = (x + x)/2 = x bit for bit: the
   // symmetrisation is the identity and is not executed.
-  if (li < 12) {
-    const int r = li;
-    for (int c = 0; c < 12; ++c) {
-      double ata = 0.0;
-      for (int k = 0; k < 6; ++k) ata += PA[r * 6 + k] * PA[c * 6 + k];
-      PG[c * 12 + r] = 2.0 * (a.alpha * ata + (r == c ? (a.beta + a.gamma) : 0.0));
+#pragma unroll
+  for (int v = 0; v < VL; ++v) {
+    const int r = li + GW * v;
+    if (r < 12) {
+      for (int c = 0; c < 12; ++c) {
+        double ata = 0.0;
+        for (int k = 0; k < 6; ++k) ata += PA[r * 6 + k] * PA[c * 6 + k];
+        PG[c * 12 + r] = 2.0 * (a.alpha * ata + (r == c ? (a.beta + a.gamma) : 0.0));
+      }
     }
   }
   GI_SYNC();
-  if (li < 12) {
-    const int r = li;
-    double atf = 0.0;
-    const double *FT = a.FT_total_des + inst * 6;
-    for (int k = 0; k < 6; ++k) atf += PA[r * 6 + k] * FT[k];
-    P.g0[r] = -2.0 * (a.alpha * atf + a.beta * guess + a.gamma * a.grf_opt[inst * 12 + r]);
+#pragma unroll
+  for (int v = 0; v < VL; ++v) {
+    const int r = li + GW * v;
+    if (r < 12) {
+      double atf = 0.0;
+      const double *FT = a.FT_total_des + inst * 6;
+      for (int k = 0; k < 6; ++k) atf += PA[r * 6 + k] * FT[k];
+      Pg0[r] = -2.0 * (a.alpha * atf + a.beta * guess[v] + a.gamma * a.grf_opt[inst * 12 + r]);
+    }
   }
   GI_SYNC();
   // swing-leg equality pattern AA (:310-350)
   const int pat = force_pattern(a.mode[inst], a.right_support[inst]);
   double f;
   int st, it;
-  gi_solve_group(P.gi, li, 12, 12, 24, PG, 12, P.g0, c_force_CE[pat], c_force_zeros,
+  gi_solve_group<GW>(P.gi, li, 12, 12, 24, PG, 12, Pg0, c_force_CE[pat], c_force_zeros,
                  ForceCi{a.mu, a.fz_max}, P.gi.x,
                  f, st, it);
   GI_SYNC();
   // QPBaseClass::solveQP: success iff no NaN (go1_rt_control QPBaseClass.cpp:116-142); Solve / fallback
   bool ok = true;
   for (int k = 0; k < 12; ++k) ok = ok && !isnan(P.gi.x[k]);
-  if (li < 12) {
-    a.grf_opt[inst * 12 + li] = ok ? P.gi.x[li] : guess;
-    a.F_leg_guess[inst * 12 + li] = guess;
-    a.F_leg_ref[inst * 12 + li] = guess;  // = Fref (F_leg_guess := F_leg_ref, :251-260)
+#pragma unroll
+  for (int v = 0; v < VL; ++v) {
+    const int r = li + GW * v;
+    if (r < 12) {
+      a.grf_opt[inst * 12 + r] = ok ? P.gi.x[r] : guess[v];
+      a.F_leg_guess[inst * 12 + r] = guess[v];
+      a.F_leg_ref[inst * 12 + r] = guess[v];  // = Fref (F_leg_guess := F_leg_ref, :251-260)
+    }
   }
   if (li == 0) {
     if (a.qp_solution) a.qp_solution[inst] = ok ? 1 : 0;
@@ -398,6 +419,21 @@ extern "C" void qloco_force_params_default(qloco_force_params *p) {
 }
 
 // c_force_CE, once per device
+// Robots per wave: eight 8-lane groups for the grouped launch, four 16-lane
+// groups for the ungrouped one (eight robots in arbitrary order diverge more
+// than four: 0.77 vs 0.74 ms ungrouped, 0.41 vs 0.44 ms grouped at 65,536
+// robots, profiles/r6y_force_qp_group_width_ab.txt).  The results are
+// bit-identical either way (qloco_gi_core.hpp); QLOCO_FORCE_GW=8 / 16 forces
+// one width for A/B measurements.
+static int force_group_width(bool grouped) {
+  static const int forced = [] {
+    const char *e = getenv("QLOCO_FORCE_GW");
+    const int v = e ? atoi(e) : 0;
+    return (v == 8 || v == 16) ? v : 0;
+  }();
+  return forced ? forced : (grouped ? 8 : 16);
+}
+
 static int force_ce_upload() {
   static std::mutex mu;
   static bool done[256] = {};
@@ -481,8 +517,13 @@ extern "C" int qloco_force_qp_solve_ordered(const qloco_force_params *prm, int64
     a.list = list;
     a.prev_it = prev;
   }
-  const unsigned blocks = (unsigned)((batch + GI_GROUPS - 1) / GI_GROUPS);
-  hipLaunchKernelGGL(force_qp_kernel, dim3(blocks), dim3(64), 0, st, a);
+  if (force_group_width(a.list != nullptr) == 16) {
+    const unsigned blocks = (unsigned)((batch + 3) / 4);
+    hipLaunchKernelGGL(force_qp_kernel<16>, dim3(blocks), dim3(64), 0, st, a);
+  } else {
+    const unsigned blocks = (unsigned)((batch + 7) / 8);
+    hipLaunchKernelGGL(force_qp_kernel<8>, dim3(blocks), dim3(64), 0, st, a);
+  }
   QLOCO_HIP_CHECK(hipGetLastError(), "force_qp_kernel launch");
   return QLOCO_OK;
 }

@@ -118,3 +118,18 @@ def test_two_wave_literal_kernel_budget(kernels):
         assert k[".vgpr_count"] + k[".agpr_count"] <= 256, (name, k[".vgpr_count"])
         assert k[".group_segment_fixed_size"] <= 40960, (name, k[".group_segment_fixed_size"])
         assert k[".vgpr_spill_count"] == 0 and k[".private_segment_fixed_size"] == 0, name
+
+
+# the force QP: 8-lane groups (grouped launch) and 16-lane
+# groups (ungrouped), both spill-free at two waves' register budget; the
+# 8-robot block's LDS lets six blocks share a CU's 160 KB
+FORCE_GW8 = "_ZN5qloco15force_qp_kernelILi8EEEvNS_9ForceArgsE"
+FORCE_GW16 = "_ZN5qloco15force_qp_kernelILi16EEEvNS_9ForceArgsE"
+
+
+def test_force_qp_kernel_budget(kernels):
+    for name in (FORCE_GW8, FORCE_GW16):
+        k = kernels[name]
+        assert k[".vgpr_count"] + k[".agpr_count"] <= 256, (name, k[".vgpr_count"])
+        assert k[".vgpr_spill_count"] == 0 and k[".private_segment_fixed_size"] == 0, name
+    assert 6 * kernels[FORCE_GW8][".group_segment_fixed_size"] <= 160 * 1024
