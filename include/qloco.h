@@ -294,6 +294,14 @@ int qloco_force_qp_solve_ordered(const qloco_force_params *prm, int64_t batch,
  * fields as qloco_force_params_default (the sim copy: mass 12, mu 0.25). */
 void qloco_force_params_hw(qloco_force_params *p);
 
+/* Robots per wavefront of the force-QP kernel: 8 (eight 8-lane groups, the
+ * default) or 16 (four 16-lane groups).  The outputs are bit-identical
+ * either way; the knob exists for A/B measurements and the test that pins
+ * that identity (QLOCO_FORCE_GW=16 in the environment sets the initial
+ * value).  Returns the previous width, or QLOCO_ERR_ARG for other values.
+ * Process-wide; set it while no force-QP launch is being enqueued. */
+int qloco_force_set_group_width(int gw);
+
 /* The hardware loop's feed-forward after force_opt (unitree_legged_real
  * torque_mode.cpp:1370-1384): rate = min((dynamic_count / 500)^2, 1),
  * F_opt = rate (grf_opt - grf_base) + grf_base per leg (grf_base: the

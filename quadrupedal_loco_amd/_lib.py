@@ -87,6 +87,7 @@ SIGNATURES = {
     "qloco_leg_ik": (C.c_int, [i64] + [vp] * 10),
     "qloco_joint_torques": (C.c_int, [i64] + [vp] * 9),
     "qloco_force_params_hw": (None, [C.POINTER(ForceParams)]),
+    "qloco_force_set_group_width": (C.c_int, [C.c_int]),
     "qloco_hw_torque_ff": (C.c_int, [i64] + [vp] * 6),
     "qloco_body_state_init_host": (C.c_int, [i64, vp]),
     "qloco_body_mpc_step": (C.c_int, [i64] + [vp] * 10),

@@ -151,7 +151,7 @@ __constant__ BodyConsts c_body_K;
 
 struct BodyLds {
   struct Grp {
-    double g0[BNT], ci0[BNI], x[BNT];  // G is built in gi.R (see qloco_gi_core.hpp)
+    double g0[BNT], ci0[BNI], x[BNT];  // G is built in gi.J (read once, before J is formed)
     GiLdsT<BNT, BNI, 0> gi;
   } g[GI_GROUPS];
 };
@@ -245,10 +245,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
                         K.beltathetax / 2 * K.ppu_2[c * BNH + r] + K.gama_zmpy / 2 * pp;
       const double wy = K.Rthetay / 2 * I + K.alphathetay / 2 * K.pvu_2[c * BNH + r] +
                         K.beltathetay / 2 * K.ppu_2[c * BNH + r] + K.gama_zmpx / 2 * pp;
-      P.gi.R[c * BNT + r] = 2 * wx;
-      P.gi.R[(c + BNH) * BNT + (r + BNH)] = 2 * wy;
-      P.gi.R[c * BNT + (r + BNH)] = 0.0;
-      P.gi.R[(c + BNH) * BNT + r] = 0.0;
+      P.gi.J[c * BNT + r] = 2 * wx;
+      P.gi.J[(c + BNH) * BNT + (r + BNH)] = 2 * wy;
+      P.gi.J[c * BNT + (r + BNH)] = 0.0;
+      P.gi.J[(c + BNH) * BNT + r] = 0.0;
     }
     if (li < BNT) {  // q_goal row li (:523-526): x rows 0..3, y rows 4..7
       const int r = li & 3;
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
     GI_SYNC();
     double f;
     int it;
-    gi_solve_group(P.gi, li, BNT, 0, BNI, P.gi.R, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
+    gi_solve_group(P.gi, li, BNT, 0, BNI, P.gi.J, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
                    status, it);
     GI_SYNC();
     if (li == 0) {

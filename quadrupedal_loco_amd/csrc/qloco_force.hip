@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 
 #include "qloco_gi_core.hpp"
@@ -53,15 +54,16 @@ static_assert(kForceClasses == QLOCO_FORCE_CLASSES, "qloco_common.hpp");
 // 12x12 column-major, in constant memory (identical for every robot).
 __constant__ double c_force_CE[5][144];
 
-// Per group: A (6x12) is built in the solver's J and G in its R (both are
-// free until the solve starts, and the solver reads only G's lower triangle,
-// copying it in place); g0 lives in the solver's z (first written by
+// Per group: A (6x12) is built in the solver's R and G in its J (both are
+// free until the solve starts: the solver copies G's lower triangle into R
+// before it forms J, and A is dead once G and g0 are built); g0 lives in the solver's z (first written by
 // update_z in the equality loop, after the last reads of g0: the x0 solve and
 // f = g0'x / 2); the inequality rows are generated (ForceCi), F_leg_guess
 // stays in the owning lanes' registers, ce0 is the constant zero vector and
-// the solution is read from gi.x.  With byte-sized constraint indices a
-// group needs 3.36 KB: an 8-robot block (8-lane groups) 26.9 KB, six blocks
-// per CU; a 4-robot block (16-lane groups) 13.4 KB.
+// the solution is read from gi.x.  With byte-sized constraint indices and R
+// packed (qloco_gi_core.hpp) a group needs 2.83 KB: an 8-robot block
+// (8-lane groups) 22.6 KB, seven blocks per CU; a 4-robot block (16-lane
+// groups) 11.3 KB.
 template <int FG>
 struct ForceLds {
   struct Grp {
@@ -239,8 +241,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kForceWpe)))
   if (pos >= a.batch) return;
   const int64_t inst = a.list ? a.list[pos] : pos;
   typename ForceLds<FG>::Grp &P = S.g[grp];
-  double *const PA = P.gi.J;  // A, 6x12 col-major (dead before J is formed)
-  double *const PG = P.gi.R;  // G, 12x12 col-major (the solver's LLT workspace)
+  double *const PA = P.gi.R;  // A, 6x12 col-major (dead before the solver clears R)
+  double *const PG = P.gi.J;  // G, 12x12 col-major (read once, before J is formed)
+  static_assert(sizeof(P.gi.R) >= 72 * sizeof(double), "A fits the packed R");
   double *const Pg0 = P.gi.z;  // g0 (dead before z is first written)
 
   // ---- force_distribution (state F_leg_ref in/out) -> F_leg_guess
@@ -419,19 +422,19 @@ extern "C" void qloco_force_params_default(qloco_force_params *p) {
 }
 
 // c_force_CE, once per device
-// Robots per wave: eight 8-lane groups for the grouped launch, four 16-lane
-// groups for the ungrouped one (eight robots in arbitrary order diverge more
-// than four: 0.77 vs 0.74 ms ungrouped, 0.41 vs 0.44 ms grouped at 65,536
-// robots, profiles/r6y_force_qp_group_width_ab.txt).  The results are
-// bit-identical either way (qloco_gi_core.hpp); QLOCO_FORCE_GW=8 / 16 forces
-// one width for A/B measurements.
-static int force_group_width(bool grouped) {
-  static const int forced = [] {
-    const char *e = getenv("QLOCO_FORCE_GW");
-    const int v = e ? atoi(e) : 0;
-    return (v == 8 || v == 16) ? v : 0;
-  }();
-  return forced ? forced : (grouped ? 8 : 16);
+// Robots per wave: eight 8-lane groups (force_qp_kernel<8>), grouped or not
+// (65,536 robots: 0.328 vs 0.444 ms grouped, 0.585 vs 0.742 ms ungrouped
+// against four 16-lane groups, profiles/r6aa_force_qp_group_width_ab.txt).
+// The results are bit-identical either way (qloco_gi_core.hpp);
+// qloco_force_set_group_width / QLOCO_FORCE_GW=16 select the 16-lane kernel.
+static std::atomic<int> g_force_gw{[] {
+  const char *e = getenv("QLOCO_FORCE_GW");
+  return (e && atoi(e) == 16) ? 16 : 8;
+}()};
+
+extern "C" int qloco_force_set_group_width(int gw) {
+  if (gw != 8 && gw != 16) return QLOCO_ERR_ARG;
+  return g_force_gw.exchange(gw);
 }
 
 static int force_ce_upload() {
@@ -517,7 +520,7 @@ extern "C" int qloco_force_qp_solve_ordered(const qloco_force_params *prm, int64
     a.list = list;
     a.prev_it = prev;
   }
-  if (force_group_width(a.list != nullptr) == 16) {
+  if (g_force_gw.load(std::memory_order_relaxed) == 16) {
     const unsigned blocks = (unsigned)((batch + 3) / 4);
     hipLaunchKernelGGL(force_qp_kernel<16>, dim3(blocks), dim3(64), 0, st, a);
   } else {

@@ -233,3 +233,20 @@ def test_srbd_polish_rejected_until_implemented():
     assert L.qloco_srbd_solve(C.byref(sp), 4, *dummy, None, None, None, None, None, None) == 100
     assert L.qloco_srbd_solve_ex(C.byref(sp), 4, *dummy, None, None, None, None, None, None,
                                  0, None) == 100
+
+
+def test_force_group_width_setter():
+    """qloco_force_set_group_width (host-only, no GPU call): 8 / 16 accepted
+    and the previous width returned, anything else QLOCO_ERR_ARG with the
+    width unchanged."""
+    from quadrupedal_loco_amd._lib import lib
+    L = lib()
+    prev = L.qloco_force_set_group_width(16)
+    try:
+        assert prev in (8, 16)
+        assert L.qloco_force_set_group_width(8) == 16
+        assert L.qloco_force_set_group_width(0) == 100
+        assert L.qloco_force_set_group_width(32) == 100
+        assert L.qloco_force_set_group_width(8) == 8
+    finally:
+        L.qloco_force_set_group_width(prev)

@@ -190,6 +190,38 @@ def test_force_qp_matches_restatement_over_ticks(hw, grouped):
         O.lib().qo_dyn_free(C.byref(s))
 
 
+@pytest.mark.parametrize("grouped", [True, False])
+def test_force_qp_group_width_is_bit_identical(grouped):
+    """Eight 8-lane groups per wave (the default) and four 16-lane groups run
+    the same per-element operations in the same order (qloco_gi_core.hpp):
+    every output equal bit for bit over four ticks, member state carried,
+    B = 1001 (a partial last wavefront at both widths)."""
+    from quadrupedal_loco_amd._lib import lib
+    dev = _dev()
+    L = lib()
+    rng = np.random.default_rng(12)
+    B, ticks = 1001, 4
+    a = qp.ForceQP(batch=B, device=dev, grouped=grouped)
+    b = qp.ForceQP(batch=B, device=dev, grouped=grouped)
+    prev = L.qloco_force_set_group_width(8)
+    try:
+        for tick in range(ticks):
+            inp = force_inputs(rng, B)
+            d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in inp.items()}
+            assert L.qloco_force_set_group_width(8) in (8, 16)
+            oa = a.step(**d)
+            torch.cuda.synchronize()
+            assert L.qloco_force_set_group_width(16) == 8
+            ob = b.step(**d)
+            torch.cuda.synchronize()
+            for k in ("grf_opt", "F_leg_guess", "F_leg_ref", "qp_solution", "status", "iters"):
+                assert torch.equal(oa[k], ob[k]), (tick, k)
+        assert L.qloco_force_set_group_width(4) == 100  # QLOCO_ERR_ARG, width unchanged
+        assert L.qloco_force_set_group_width(16) == 16
+    finally:
+        L.qloco_force_set_group_width(prev)
+
+
 def test_force_qp_grouped_launch_is_bit_identical():
     """qloco_force_qp_solve_ordered groups the robots by swing-leg pattern and
     previous iteration count before the launch; every robot's
