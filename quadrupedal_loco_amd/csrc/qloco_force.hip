@@ -60,10 +60,10 @@ __constant__ double c_force_CE[5][144];
 // update_z in the equality loop, after the last reads of g0: the x0 solve and
 // f = g0'x / 2); the inequality rows are generated (ForceCi), F_leg_guess
 // stays in the owning lanes' registers, ce0 is the constant zero vector and
-// the solution is read from gi.x.  With byte-sized constraint indices and R
-// packed (qloco_gi_core.hpp) a group needs 2.83 KB: an 8-robot block
-// (8-lane groups) 22.6 KB, seven blocks per CU; a 4-robot block (16-lane
-// groups) 11.3 KB.
+// the solution is read from gi.x.  With R packed and the per-constraint
+// state in registers (qloco_gi_core.hpp) a group needs 2.47 KB: an 8-robot
+// block (8-lane groups) 19.8 KB, eight blocks per CU -- the two waves per
+// SIMD the register budget allows; a 4-robot block (16-lane groups) 9.9 KB.
 template <int FG>
 struct ForceLds {
   struct Grp {
@@ -423,8 +423,8 @@ extern "C" void qloco_force_params_default(qloco_force_params *p) {
 
 // c_force_CE, once per device
 // Robots per wave: eight 8-lane groups (force_qp_kernel<8>), grouped or not
-// (65,536 robots: 0.328 vs 0.444 ms grouped, 0.585 vs 0.742 ms ungrouped
-// against four 16-lane groups, profiles/r6aa_force_qp_group_width_ab.txt).
+// (65,536 robots: 0.298 vs 0.454 ms grouped, 0.528 vs 0.778 ms ungrouped
+// against four 16-lane groups, profiles/r6ac_force_qp_group_width_ab.txt).
 // The results are bit-identical either way (qloco_gi_core.hpp);
 // qloco_force_set_group_width / QLOCO_FORCE_GW=16 select the 16-lane kernel.
 static std::atomic<int> g_force_gw{[] {
