@@ -4,7 +4,7 @@
 // PRMPCClass.cpp:379-714) + Indexfind (:716-738) + solve_body_rotation /
 // Solve (:799-849), called at 100 Hz from gait_fast.cpp:620.  Constants of
 // PRMPCClass::Initialize (:157-374) are computed once on the host
-// (body_constants) and passed by value.  One instance per 16-lane group:
+// (body_constants) and passed by value.  One instance per 8-lane group:
 // the group derives the schedule integers (bjx1, bjx2, t_yu -- fp64 compares,
 // bit-exact), builds the 8-variable QP in LDS, solves it with the
 // Goldfarb-Idnani core and applies the reference's clamping, propagation and
@@ -149,11 +149,15 @@ __constant__ double c_body_CI[BNT * BNI];
 // argument the dynamically indexed struct was materialised in VGPRs.
 __constant__ BodyConsts c_body_K;
 
+// Eight robots per wave: one 8-lane Goldfarb-Idnani group per robot, a lane
+// per variable (BNT = 8; qloco_gi_core.hpp's results do not depend on the
+// group width).
+constexpr int kBodyGW = 8, kBodyGroups = 64 / kBodyGW;
 struct BodyLds {
   struct Grp {
     double g0[BNT], ci0[BNI], x[BNT];  // G is built in gi.J (read once, before J is formed)
     GiLdsT<BNT, BNI, 0> gi;
-  } g[GI_GROUPS];
+  } g[kBodyGroups];
 };
 
 // PRMPCClass::Indexfind, xyz = 0 branch (:716-738)
@@ -166,14 +170,13 @@ __device__ __forceinline__ int indexfind(const BodyConsts &k, double goal) {
 #define R2(m, r, c) ((m)[(c)*2 + (r)])
 #define R3(m, r, c) ((m)[(c)*3 + (r)])
 
-// The LDS (11.6 KB per 4-robot block) admits 13 blocks per CU; the compiler
-// lands at 156 VGPRs (no spills) for the 2-waves/SIMD floor set here, i.e.
-// 3 waves/SIMD -- both limits agree
+// 2-waves/SIMD register floor (no spills); the LDS of an 8-robot block sets
+// the resident waves
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void body_mpc_kernel(const BodyArgs a) {
   __shared__ BodyLds S;
   const BodyConsts &K = c_body_K;
-  const int lane = threadIdx.x, grp = lane >> 4, li = lane & 15;
-  const int64_t inst = (int64_t)blockIdx.x * GI_GROUPS + grp;
+  const int lane = threadIdx.x, grp = lane / kBodyGW, li = lane % kBodyGW;
+  const int64_t inst = (int64_t)blockIdx.x * kBodyGroups + grp;
   if (inst >= a.batch) return;
   BodyLds::Grp &P = S.g[grp];
   double *st = a.state + inst * QLOCO_BODY_STATE_LEN;
@@ -195,18 +198,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
   if (active) {
     const double t_f0 = (i + 1) * K.dt_mpc, t_f3 = (i + BNH) * K.dt_mpc;  // :406
     if (a.tx) {
-      // the robot's _tx: lane li of the group holds entries li and li + 16,
-      // loaded together; Indexfind's stopping index (the first j with
-      // goal < _tx(j), 27 if none) is the lowest set bit of a ballot --
-      // the same answer as the scan for any _tx, one load round trip
+      // the robot's _tx: lane li of the group holds entries li + 8 q
+      // (q < 4), loaded together; Indexfind's stopping index (the first j
+      // with goal < _tx(j), 27 if none) is the lowest set bit of the group's
+      // ballots -- the same answer as the scan for any _tx, one load round trip
       const double *txr = a.tx + (a.tx_tile > 0 ? (inst >> 6) * a.tx_tile + (inst & 63) : inst);
-      const bool v1 = li + 16 < BSTEPS;
-      const double t0 = txr[li * a.tx_stride];
-      const double t1 = v1 ? txr[(li + 16) * a.tx_stride] : 0.0;
+      constexpr int TQ = (BSTEPS + kBodyGW - 1) / kBodyGW;
+      double tq[TQ];
+#pragma unroll
+      for (int q = 0; q < TQ; ++q) tq[q] = (li + kBodyGW * q < BSTEPS) ? txr[(li + kBodyGW * q) * a.tx_stride] : 0.0;
       auto first_below = [&](double goal) {
-        const uint64_t m0 = (__ballot(goal < t0) >> (16 * grp)) & 0xFFFFull;
-        const uint64_t m1 = (__ballot(v1 && goal < t1) >> (16 * grp)) & 0xFFFFull;
-        return m0 ? __builtin_ctzll(m0) : (m1 ? 16 + __builtin_ctzll(m1) : BSTEPS);
+        int j = BSTEPS;
+#pragma unroll
+        for (int q = TQ - 1; q >= 0; --q) {
+          const uint64_t m = (__ballot(li + kBodyGW * q < BSTEPS && goal < tq[q]) >> (kBodyGW * grp)) &
+                             ((1ull << kBodyGW) - 1);
+          if (m) j = kBodyGW * q + __builtin_ctzll(m);
+        }
+        return j;
       };
       bjx1 = first_below(t_f0);  // Indexfind + 1 = stopping index
       bjx2 = first_below(t_f3);
@@ -234,10 +243,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
     }
     double pth[BNH];
     for (int jx = 0; jx < BNH; jx++) pth[jx] = K.j_ini / (K.mass * (R3(comacc_ref, 2, jx) + K.g));
-    // QP data (:505-535), one entry set per lane of the 16-lane group (each
+    // QP data (:505-535), entry sets spread over the 8-lane group (each
     // entry computed exactly as the serial loops of the reference do)
-    {
-      const int r = li & 3, c = li >> 2;  // G: lane (r, c) of the two 4x4 blocks
+#pragma unroll
+    for (int e = li; e < 2 * kBodyGW; e += kBodyGW) {
+      const int r = e & 3, c = e >> 2;  // G: entry (r, c) of the two 4x4 blocks
       const double I = (r == c) ? 1.0 : 0.0;  // :511-515
       double pp = pth[r] * pth[c];
       if (r != c) pp = 0.0;
@@ -272,8 +282,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
                         K.gama_zmpx * (-pth[r]) * det_px;
       }
     }
-    {  // ci0 (:527-535): lane (row, block pair); entries 32..47 stay 0
-      const int row = li & 3, bp = li >> 2;
+#pragma unroll
+    for (int e = li; e < 2 * kBodyGW; e += kBodyGW) {  // ci0 (:527-535): (row, block pair); entries 32..47 stay 0
+      const int row = e & 3, bp = e >> 2;
       const double ppsx = K.pps[row] * thetaxk[0] + K.pps[BNH + row] * thetaxk[1];
       const double ppsy = K.pps[row] * thetayk[0] + K.pps[BNH + row] * thetayk[1];
       double e0, e1;
@@ -289,12 +300,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
       }
       P.ci0[(2 * bp) * BNH + row] = e0;
       P.ci0[(2 * bp + 1) * BNH + row] = e1;
-      P.ci0[8 * BNH + li] = 0.0;
+      P.ci0[8 * BNH + e] = 0.0;
     }
     GI_SYNC();
     double f;
     int it;
-    gi_solve_group(P.gi, li, BNT, 0, BNI, P.gi.J, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
+    gi_solve_group<kBodyGW>(P.gi, li, BNT, 0, BNI, P.gi.J, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
                    status, it);
     GI_SYNC();
     if (li == 0) {
@@ -367,7 +378,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
     }
   }
   GI_SYNC();
-  if (li < 14) a.com_traj[inst * 14 + li] = st[12 + li];  // :696-709 (last state otherwise)
+  for (int k = li; k < 14; k += kBodyGW) a.com_traj[inst * 14 + k] = st[12 + k];  // :696-709 (last state otherwise)
   if (li == 0 && a.status) a.status[inst] = active ? status : QLOCO_OK;
 }
 
@@ -466,7 +477,7 @@ int qloco::body_mpc_launch(int64_t batch, const int32_t *i, const double *bodyan
   a.ref_ld = ref_ld;
   const int rc = body_ci_upload(a.k);
   if (rc != QLOCO_OK) return rc;
-  const unsigned blocks = (unsigned)((batch + GI_GROUPS - 1) / GI_GROUPS);
+  const unsigned blocks = (unsigned)((batch + kBodyGroups - 1) / kBodyGroups);
   hipLaunchKernelGGL(body_mpc_kernel, dim3(blocks), dim3(64), 0, stream, a);
   QLOCO_HIP_CHECK(hipGetLastError(), "body_mpc_kernel launch");
   return QLOCO_OK;

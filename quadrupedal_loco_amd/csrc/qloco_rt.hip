@@ -15,7 +15,7 @@
 // Three launches on one stream:
 //   rt_pre_kernel    one robot per lane: everything before body_theta_mpc;
 //                    writes the body kernel's reference arrays and run mask
-//   body_mpc_kernel  4 robots per wave (16-lane Goldfarb-Idnani groups), on
+//   body_mpc_kernel  8 robots per wave (8-lane Goldfarb-Idnani groups), on
 //                    each robot's own _tx schedule
 //   rt_post_kernel   one robot per lane: packs /rtMPC/traj, /rt2nrt/state
 //

@@ -69,8 +69,12 @@ def _traj_metrics(u, ref, x0, xr, ft, ct, N):
 # one (measured max 0.20 N, p99 0.05-0.17 N over 2,765 such instances at
 # N = 10 / 16 / 20, profiles/r5c_literal_parity_scan.txt); where fp32 passes
 # a check one interval earlier or later the runs stop at two eps-optimal
-# points and |du0|_inf <= 40 N (measured max 22.8 N over 19 such instances).
-U0_SAME_NEAR, U0_SAME_ALL, U0_APART = 0.5, 2.0, 40.0
+# points and |du0|_inf <= 30 N (measured max 22.8 N over 19 such instances;
+# round 6: 40 -> 30 N, ADVICE r5 -- at the GPU's own iteration count the
+# restatement is no closer, profiles/r6v_u0_at_gpu_stop_probe.txt, so the
+# certificate for these points is OSQP's termination test,
+# test_srbd_literal_iterate_passes_osqp_termination).
+U0_SAME_NEAR, U0_SAME_ALL, U0_APART = 0.5, 2.0, 30.0
 
 
 class U0Bound:
@@ -958,7 +962,7 @@ def test_srbd_literal_iterate_passes_osqp_termination(N, B, gait, wset):
     termination test re-evaluated in float64 on the reference's unscaled QP
     (_osqp_termination), whether or not it stops at the same check as the
     fp64 restatement -- the criterion, not a u0 distance, is what certifies
-    the instances that stop one check apart (U0Bound's 40 N).  The unscaled
+    the instances that stop one check apart (U0Bound's 30 N).  The unscaled
     y comes from the warm_start = 1 form of the same call started from zeros
     (x = y = z = 0 is the cold start): its iterations equal the cold
     launch's and its u0 agrees to rounding.  Reports the instances one check
