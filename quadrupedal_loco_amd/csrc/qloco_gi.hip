@@ -6,9 +6,12 @@
 // p = 12, m = 24; dynmics_compute.cpp:265-445) and the body-inclination QP
 // (n = 8, p = 0, m = 48; PRMPCClass.cpp:799-849).
 //
-// Mapping: one QP instance per 16-lane group, four per wavefront (one
-// wavefront per workgroup).  J, R and the vectors live in LDS; lane i of a
-// group owns row/column/constraint i in the vector steps.  Control flow is
+// Mapping (this generic kernel): one QP instance per 16-lane group, four per
+// wavefront (one wavefront per workgroup); the force and body kernels use
+// 8-lane groups (qloco_gi_core.hpp: the results do not depend on the width).
+// J, R (packed) and the vectors live in LDS, s(x) and the active-set
+// snapshots in registers; lane i of a group owns row/column/constraint
+// i, i + GW, ... in the vector steps.  Control flow is
 // the reference's goto machine (l1/l2/l2a), uniform inside a group; groups
 // of one wave may diverge (exec masking).  Double precision, compiled with
 // -ffp-contract=off, and every dot product is summed by ONE lane in the
