@@ -222,6 +222,41 @@ def test_force_qp_group_width_is_bit_identical(grouped):
         L.qloco_force_set_group_width(prev)
 
 
+def test_force_qp_grouped_launch_replays_from_a_hip_graph():
+    """The grouped force-QP call (memset + count + scatter + force kernel,
+    INTEGRATION.md §2) allocates nothing and keeps its state in caller
+    buffers, so it can be captured once and replayed every servo tick: a
+    captured ForceQP.step fed new inputs through static tensors gives the
+    eager call's outputs bit for bit over four ticks, member state and
+    grouping state carried by both."""
+    dev = _dev()
+    rng = np.random.default_rng(13)
+    B, ticks = 1001, 4
+    ticks_in = [{k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in force_inputs(rng, B).items()}
+                for _ in range(ticks)]
+    static = {k: v.clone() for k, v in ticks_in[0].items()}
+    eager = qp.ForceQP(batch=B, device=dev)
+    graphed = qp.ForceQP(batch=B, device=dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):  # warm-up on a throw-away instance: constants uploaded
+        qp.ForceQP(batch=B, device=dev).step(**static)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        og = graphed.step(**static)
+    for tick in range(ticks):
+        for k, v in ticks_in[tick].items():
+            static[k].copy_(v)
+        g.replay()
+        oe = eager.step(**ticks_in[tick])
+        torch.cuda.synchronize()
+        for k in ("grf_opt", "F_leg_guess", "F_leg_ref", "qp_solution", "status", "iters"):
+            assert torch.equal(og[k], oe[k]), (tick, k)
+        # the carried iteration counts (the list's order inside a class is immaterial)
+        assert torch.equal(graphed.order_ws[:B], eager.order_ws[:B]), tick
+
+
 def test_force_qp_grouped_launch_is_bit_identical():
     """qloco_force_qp_solve_ordered groups the robots by swing-leg pattern and
     previous iteration count before the launch; every robot's
