@@ -305,7 +305,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void bo
     GI_SYNC();
     double f;
     int it;
-    gi_solve_group<kBodyGW>(P.gi, li, BNT, 0, BNI, P.gi.J, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
+    // the serial l2 scan: the butterfly's registers would cost this kernel
+    // its third wave per SIMD (176 VGPRs; rt tick +1.3 %, profiles/r6am_gi_l2_butterfly_ab.txt)
+    gi_solve_group<kBodyGW, false>(P.gi, li, BNT, 0, BNI, P.gi.J, BNT, P.g0, nullptr, nullptr, c_body_CI, P.ci0, P.x, f,
                    status, it);
     GI_SYNC();
     if (li == 0) {
